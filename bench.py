@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X path tracer.
+
+Metric (BASELINE.json): Mpaths/s at 1920x1080, 4 bounces (config C2:
+cornellbox, 64 spp, L = 4, diffuse).  One "step" = one complete C2 render:
+reset + 64 frames (1 spp each, L bounce launches per frame) on the tiles this
+rank owns, plus — for N > 1 — the single RCCL reduce of the RGBA32F
+accumulation image to rank 0.  value = paths of all ranks / max-over-ranks
+step time (strong scaling: the frame is split into 64x64 tiles, tile t on
+rank t % N).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+For N > 1 launch with torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "metal-renderer_amd"))
+
+METRIC = "Mpaths/s at 1920×1080, 4 bounces; achieved HBM GB/s vs peak; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+B_PATH, B_BOUNCE = 112, 312    # algorithmic bytes per path / per active ray-bounce
+
+CONFIGS = {
+    # BASELINE.json configs[1] — the metric's config
+    "c2": dict(workload="C2 cornellbox 1920x1080 64spp L=4 (diffuse BSDF)", scene="cornellbox", mtl=None,
+               width=1920, height=1080, spp=64, L=4, procedural=0),
+    # configs[2]: CornellBox-Water-plastic (plastic + mirror + water), 256 spp, L = 8
+    "c3": dict(workload="C3 CornellBox-Water-plastic 1920x1080 256spp L=8", scene="CornellBox-Water-plastic",
+               mtl=None, width=1920, height=1080, spp=256, L=8, procedural=0),
+    # configs[3]: 1M-triangle procedural mesh in the cornellbox shell, 64 spp, L = 4
+    "c4": dict(workload="C4 1M-triangle procedural mesh 1920x1080 64spp L=4", scene="cornellbox", mtl=None,
+               width=1920, height=1080, spp=64, L=4, procedural=1 << 20),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--precise", action="store_true", help="time the parity build instead of the fast build")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-frames", type=int, default=4, help="frames of the workload timed on the CPU oracle")
+    p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, frames):
+    """The CPU oracle (scalar C++ restatement, oracle/) on a bounded sample:
+    the first `frames` frames of the same workload, std::thread over rows."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/baseline infrastructure only (see oracle/mrt_oracle.cpp header)
+    import mrt
+    if not os.path.exists(oracle.LIB_PATH):
+        oracle.build()
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+    if cfg["procedural"]:
+        return None   # brute-force oracle on 1M triangles is not a bounded sample
+    sc = oracle.OracleScene(mrt.scene_path(cfg["scene"]), cfg["mtl"])
+    W, H = cfg["width"], cfg["height"]
+    t0 = time.perf_counter()
+    _, _ = sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(W * H * frames / dt / 1e6, 3), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": f"frames 0-{frames - 1} of the workload ({W}x{H}, L={cfg['L']}, {W * H * frames} paths), "
+                      f"brute-force nearest hit, {threads} std::threads over rows, {dt:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    cfg = CONFIGS[args.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    import torch
+    import torch.distributed as dist
+    import mrt
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
+    scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=local_rank)
+    image = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True, shard_rank=rank, shard_count=world,
+                     stream=stream.cuda_stream, image_ptr=image.data_ptr())
+    r.prepare(spp)
+
+    def step():
+        r.reset()
+        r.draw(spp)
+        if world > 1:
+            dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
+
+    for _ in range(args.warmup):
+        step()
+    r.sync()
+    torch.cuda.synchronize()
+    base = r.stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    r.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = r.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([st["active_ray_bounces"] - base["active_ray_bounces"], st["paths"] - base["paths"],
+                            st["kernel_launches"] - base["kernel_launches"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot)
+    total_paths = W * H * spp * args.steps
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_paths / elapsed / 1e6
+
+    # roofline of the dominant kernel (the fused bounce kernel; every launch of
+    # the frame is one) from HIP events recorded around each launch on the
+    # renderer's stream, over the timed steps of this rank
+    A = st["active_ray_bounces"] - base["active_ray_bounces"]
+    P = st["paths"] - base["paths"]
+    launches = st["kernel_launches"] - base["kernel_launches"]
+    kms = st["kernel_ms"] - base["kernel_ms"]
+    bytes_alg = B_PATH * P + B_BOUNCE * A
+    avg_launch_ms = kms / max(1, launches)
+    achieved = (bytes_alg / max(1, launches)) / (avg_launch_ms * 1e-3) / 1e9 if launches else 0.0
+    traffic = None
+    pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mpaths/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"reference scene renderer/Media/{cfg['scene']}.obj" +
+                (f" + seeded procedural mesh ({cfg['procedural']} tris)" if cfg["procedural"] else "") +
+                ", deterministic noise seed",
+        "config": {"workload": cfg["workload"], "width": W, "height": H, "spp": spp, "max_path_length": L,
+                   "scene": cfg["scene"], "parallelism": f"tiles64x{world}" + (" + rccl reduce" if world > 1 else ""),
+                   "build": "precise" if args.precise else "fast"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "bounce_kernel", "launches": launches, "avg_launch_ms": round(avg_launch_ms, 4),
+                     "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
+                     "active_ray_bounces_per_step": int(A / max(1, args.steps))},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+/*
+ * mrt.h — C ABI of the MI355X-native path tracer (libmrt.so).
+ *
+ * This is the drop-in boundary for the hot path of serhii-rieznik/metal-renderer.
+ * The reference exposes the path through two boundaries, both reproduced here:
+ *
+ *   B-1  App <-> renderer:  the Objective-C `Renderer` (renderer/Renderer.h:3-8)
+ *        -initWithMetalKitView:            -> mrt_renderer_create
+ *        -mtkView:drawableSizeWillChange:  -> mrt_renderer_resize   (Renderer.mm:640-657)
+ *        -drawInMTKView:                   -> mrt_renderer_draw     (Renderer.mm:587-638)
+ *        -saveCurrentImage                 -> mrt_renderer_save_image (Renderer.mm:659-662;
+ *                                             a working save, the reference's is a stub)
+ *        window-title stats                -> mrt_renderer_stats    (Renderer.mm:631-637)
+ *   B-2  Renderer <-> GPU:  the per-stage dispatches of performRaytracing:
+ *        (renderer/Renderer.mm:500-585) over the reference AoS records
+ *        (renderer/Raytracing.h:47-123):
+ *        rayGenerator        (Shaders.metal:75-103)   -> mrt_raygen
+ *        MPS nearest-hit     (Renderer.mm:519-523,545-553; config :464-469)
+ *                                                     -> mrt_intersect
+ *        MPS rebuild         (Renderer.mm:456-462)    -> mrt_scene_create (BVH build)
+ *        intersectionHandler (Shaders.metal:105-212)  -> mrt_shade
+ *        lightSamplingHandler(Shaders.metal:214-231)  -> mrt_resolve_shadow
+ *        accumulateImage     (Shaders.metal:233-249)  -> mrt_accumulate
+ *
+ * Conventions: every function returns 0 on success and a negative mrt_status
+ * on failure; mrt_last_error() returns a thread-local message.  No exception
+ * crosses the ABI.  Handles are opaque.  A handle is externally synchronised
+ * (one caller thread at a time, like the MTKView main thread).  Device
+ * pointers are HIP device memory on the handle's device; `stream` arguments
+ * are hipStream_t (NULL = the handle's own stream).
+ * Image layout: RGBA32F, W*H*4 floats, row 0 = BOTTOM of the view (the
+ * reference's texture orientation, Shaders.metal:81,94).
+ */
+#ifndef MRT_H_
+#define MRT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRT_ABI_VERSION 1
+
+typedef enum mrt_status {
+  MRT_OK = 0,
+  MRT_ERR_INVALID = -1,   /* bad argument */
+  MRT_ERR_IO = -2,        /* scene / image file error */
+  MRT_ERR_HIP = -3,       /* HIP runtime error (no device, launch failure, ...) */
+  MRT_ERR_NOMEM = -4,
+  MRT_ERR_STATE = -5      /* call not valid in the handle's current state */
+} mrt_status;
+
+/* flags */
+#define MRT_FLAG_PRECISE 1u   /* parity kernels: IEEE div/sqrt, no FMA contraction, CR sin/cos */
+#define MRT_FLAG_PROFILE 2u   /* time every bounce launch with HIP events (mrt_stats.kernel_ms) */
+
+typedef struct mrt_scene mrt_scene;
+typedef struct mrt_renderer mrt_renderer;
+
+/* ---- scene (initRaytracing: Renderer.mm:255-470) ------------------------ */
+typedef struct mrt_scene_desc {
+  const char* obj_path;            /* OBJ scene (renderer/Media/<name>.obj) */
+  const char* mtl_override;        /* optional .mtl used instead of the OBJ's mtllib (NULL/"" = none) */
+  uint32_t procedural_triangles;   /* >0: append a seeded displaced sphere of this many triangles */
+  uint64_t procedural_seed;
+  uint32_t max_leaf_size;          /* BVH leaf size, 0 = default (4) */
+  uint32_t lds_nodes;              /* top BVH nodes staged in LDS, 0 = default; UINT32_MAX = none */
+  int device;                      /* HIP device ordinal; -1 = host only (import + BVH, no upload) */
+} mrt_scene_desc;
+
+typedef struct mrt_scene_info {
+  uint32_t vertices, triangles, materials, light_triangles;
+  uint32_t bvh_nodes, bvh_leaves, bvh_depth, bvh_lds_nodes;
+  double bvh_sah_cost;
+  double build_ms;                 /* host BVH build time */
+  uint64_t device_bytes;           /* scene + BVH bytes resident on the device */
+} mrt_scene_info;
+
+int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out);
+int mrt_scene_info_get(const mrt_scene* scene, mrt_scene_info* info);
+/* Copy the flattened reference-layout buffers to host memory (any pointer may
+ * be NULL): Vertex[24 B], uint32 indices, Material[32 B], TriangleReference[20 B],
+ * LightTriangle[100 B] (light_triangles + 1 entries, the sentinel last). */
+int mrt_scene_export(const mrt_scene* scene, void* vertices, void* indices, void* materials,
+                     void* references, void* lights);
+int mrt_scene_destroy(mrt_scene* scene);
+/* Structural check of the built BVH (host): every primitive in exactly one
+ * leaf, every child box contains its subtree's triangles, depth within the
+ * traversal stack.  0 = valid. */
+int mrt_scene_check_bvh(const mrt_scene* scene);
+
+/* ---- stage-level ABI (B-2), reference AoS layouts, device pointers ------- */
+/* rayGenerator over a W x H grid: noise = 64*64 float4 (one noise slot). */
+int mrt_raygen(const mrt_scene* scene, uint32_t width, uint32_t height, const float* noise,
+               void* rays /* Ray[W*H], 80 B */, uint32_t flags, void* stream);
+/* MPS nearest-hit: records of `stride` bytes whose first 32 B are
+ * (origin, minDistance, direction, maxDistance); cull none; distance = -1 on
+ * miss or maxDistance < 0; ties -> lowest primitive index. */
+int mrt_intersect(const mrt_scene* scene, const void* rays, uint32_t stride, uint32_t count,
+                  void* intersections /* Intersection[count], 16 B */, uint32_t flags, void* stream);
+/* intersectionHandler for iteration with SharedData.frameIndex = frame_index
+ * and MAX_PATH_LENGTH = max_path_length; noise = the slot bound at index 8. */
+int mrt_shade(const mrt_scene* scene, uint32_t width, uint32_t height, uint32_t frame_index,
+              uint32_t max_path_length, const float* noise, const void* intersections, void* rays,
+              void* shadow_rays /* LightSamplingRay[W*H], 48 B */, uint32_t flags, void* stream);
+int mrt_resolve_shadow(const mrt_scene* scene, uint32_t count, const void* intersections, void* rays,
+                       const void* shadow_rays, uint32_t flags, void* stream);
+int mrt_accumulate(const mrt_scene* scene, uint32_t width, uint32_t height, uint32_t frame_index,
+                   const void* rays, float* image_rgba, uint32_t flags, void* stream);
+
+/* ---- renderer (B-1) ------------------------------------------------------ */
+typedef struct mrt_renderer_desc {
+  const mrt_scene* scene;          /* not owned; must outlive the renderer */
+  uint32_t width, height;          /* the reference's W,H = CONTENT_SCALE * drawable */
+  uint32_t max_path_length;        /* MAX_PATH_LENGTH (Raytracing.h:23), 1..64 */
+  uint64_t seed;                   /* replaces the clock seed (Renderer.mm:109,486) */
+  uint32_t shard_rank;             /* 64x64 tile t is rendered iff t % shard_count == shard_rank */
+  uint32_t shard_count;            /* 0 or 1 = the whole frame */
+  uint32_t flags;                  /* MRT_FLAG_* */
+  void* stream;                    /* optional external hipStream_t (NULL = own stream) */
+  float* image;                    /* optional external device image (W*H*4 floats), else owned */
+} mrt_renderer_desc;
+
+typedef struct mrt_stats {
+  uint64_t frame_index;            /* frames accumulated since create/resize/reset */
+  uint64_t paths;                  /* pixel paths traced by this renderer (owned pixels x frames) */
+  uint64_t active_ray_bounces;     /* A: rays alive at the start of each bounce, summed */
+  double last_draw_ms;             /* GPU time of the last draw/draw_n (HIP events) */
+  double mpaths_per_s;             /* paths of the last draw / last_draw_ms */
+  uint64_t kernel_launches;        /* bounce launches timed (MRT_FLAG_PROFILE) */
+  double kernel_ms;                /* summed bounce-kernel time (MRT_FLAG_PROFILE) */
+  uint64_t owned_pixels;
+} mrt_stats;
+
+int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);
+/* drawableSizeWillChange: reallocate, frameIndex = 0 (Renderer.mm:640-657) */
+int mrt_renderer_resize(mrt_renderer* r, uint32_t width, uint32_t height);
+/* frameIndex = 0 without reallocating (the next frame overwrites the image) */
+int mrt_renderer_reset(mrt_renderer* r);
+/* Generate + upload the noise tables for frames [frame_index, frame_index+n)
+ * ahead of time (the reference regenerates one slot per frame on the CPU,
+ * Renderer.mm:486-496).  draw_n calls it itself when needed. */
+int mrt_renderer_prepare(mrt_renderer* r, uint32_t n);
+/* One frame: 1 spp, MAX_PATH_LENGTH bounces, running-mean accumulation. */
+int mrt_renderer_draw(mrt_renderer* r);
+int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n);
+/* Wait for all queued work of the renderer. */
+int mrt_renderer_sync(mrt_renderer* r);
+/* Device pointer of the accumulation image (for an RCCL reduce). */
+int mrt_renderer_image(mrt_renderer* r, float** device_image);
+/* Synchronise and copy the image to host memory (rgba must hold W*H*4 floats). */
+int mrt_renderer_read_image(mrt_renderer* r, float* rgba, size_t count);
+/* Save the image top-down as .pfm (float RGB) or .exr (float RGBA, uncompressed). */
+int mrt_renderer_save_image(mrt_renderer* r, const char* path);
+int mrt_renderer_stats(const mrt_renderer* r, mrt_stats* stats);
+int mrt_renderer_destroy(mrt_renderer* r);
+
+/* ---- misc ----------------------------------------------------------------- */
+const char* mrt_last_error(void);
+int mrt_abi_version(void);
+/* The deterministic noise table of SURVEY.md A.3 for frame `frame` (-1 = the
+ * initial table), 64*64*4 floats, host memory. */
+int mrt_noise_table(uint64_t seed, int64_t frame, float* out16384);
+/* Number of HIP devices visible (0 when none; never fails). */
+int mrt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRT_H_ */

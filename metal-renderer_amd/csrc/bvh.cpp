@@ -1,0 +1,274 @@
+// bvh.cpp — binned-SAH BVH2 builder.  See bvh.h.
+#include "bvh.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <deque>
+
+namespace mrt {
+namespace {
+
+struct Box {
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
+  float hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  void grow(const float p[3]) {
+    for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
+  }
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
+  }
+  bool valid() const { return lo[0] <= hi[0]; }
+  float area() const {
+    if (!valid()) return 0.0f;
+    const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct BuildNode {
+  Box box;
+  int32_t child[2] = {-1, -1};   // build-node ids, -1 for leaves
+  uint32_t first = 0, count = 0; // leaf range in `order`
+  uint32_t depth = 0;
+};
+
+struct Builder {
+  const BvhBuildOptions& opt;
+  std::vector<Box> prim_box;
+  std::vector<float> centroid;      // 3 per prim
+  std::vector<uint32_t> order;
+  std::vector<BuildNode> nodes;
+  uint32_t max_depth = 0;
+  std::string err;
+
+  explicit Builder(const BvhBuildOptions& o) : opt(o) {}
+
+  // returns build-node id
+  int32_t build(uint32_t first, uint32_t count, uint32_t depth) {
+    const int32_t id = (int32_t)nodes.size();
+    nodes.emplace_back();
+    Box box, cbox;
+    for (uint32_t i = first; i < first + count; ++i) {
+      box.grow(prim_box[order[i]]);
+      cbox.grow(&centroid[3 * order[i]]);
+    }
+    nodes[id].box = box;
+    nodes[id].depth = depth;
+    const float leaf_cost = (float)count;
+    const bool depth_limited = depth + 1 >= (uint32_t)kMaxBvhDepth;
+    if (count <= 1 || (depth_limited && count <= (uint32_t)kMaxLeafSize)) {
+      make_leaf(id, first, count, depth);
+      return id;
+    }
+    if (depth_limited) { err = "BVH depth limit reached with an oversize leaf"; make_leaf(id, first, count, depth); return id; }
+
+    // binned SAH over the centroid bounds
+    const uint32_t B = std::max<uint32_t>(4, opt.bins);
+    int best_axis = -1;
+    uint32_t best_split = 0;
+    float best_cost = FLT_MAX;
+    std::vector<Box> bin_box(B);
+    std::vector<uint32_t> bin_cnt(B);
+    std::vector<float> right_area(B);
+    std::vector<uint32_t> right_cnt(B);
+    for (int axis = 0; axis < 3; ++axis) {
+      const float ext = cbox.hi[axis] - cbox.lo[axis];
+      if (!(ext > 0.0f)) continue;
+      const float scale = (float)B / ext;
+      std::fill(bin_box.begin(), bin_box.end(), Box());
+      std::fill(bin_cnt.begin(), bin_cnt.end(), 0u);
+      for (uint32_t i = first; i < first + count; ++i) {
+        const uint32_t p = order[i];
+        uint32_t b = (uint32_t)((centroid[3 * p + axis] - cbox.lo[axis]) * scale);
+        b = std::min(b, B - 1);
+        bin_box[b].grow(prim_box[p]);
+        bin_cnt[b]++;
+      }
+      Box acc;
+      uint32_t cnt = 0;
+      for (uint32_t b = B - 1; b > 0; --b) {
+        acc.grow(bin_box[b]);
+        cnt += bin_cnt[b];
+        right_area[b] = acc.area();
+        right_cnt[b] = cnt;
+      }
+      acc = Box();
+      cnt = 0;
+      for (uint32_t b = 0; b + 1 < B; ++b) {
+        acc.grow(bin_box[b]);
+        cnt += bin_cnt[b];
+        const uint32_t rc = right_cnt[b + 1];
+        if (cnt == 0 || rc == 0) continue;
+        const float cost = acc.area() * (float)cnt + right_area[b + 1] * (float)rc;
+        if (cost < best_cost) { best_cost = cost; best_axis = axis; best_split = b + 1; }
+      }
+    }
+    const float parent_area = box.area();
+    const float split_cost = parent_area > 0.0f ? opt.traversal_cost + best_cost / parent_area : FLT_MAX;
+    uint32_t mid;
+    if (best_axis < 0) {
+      // all centroids coincide: leaf if it fits, else split the range in half
+      if (count <= opt.max_leaf_size) { make_leaf(id, first, count, depth); return id; }
+      mid = first + count / 2;
+    } else {
+      if (count <= opt.max_leaf_size && leaf_cost <= split_cost) { make_leaf(id, first, count, depth); return id; }
+      const float scale = (float)B / (cbox.hi[best_axis] - cbox.lo[best_axis]);
+      const float lo = cbox.lo[best_axis];
+      auto it = std::partition(order.begin() + first, order.begin() + first + count, [&](uint32_t p) {
+        uint32_t b = (uint32_t)((centroid[3 * p + best_axis] - lo) * scale);
+        return std::min(b, B - 1) < best_split;
+      });
+      mid = (uint32_t)(it - order.begin());
+      if (mid == first || mid == first + count) mid = first + count / 2;
+    }
+    const int32_t l = build(first, mid - first, depth + 1);
+    const int32_t r = build(mid, first + count - mid, depth + 1);
+    nodes[id].child[0] = l;
+    nodes[id].child[1] = r;
+    return id;
+  }
+
+  void make_leaf(int32_t id, uint32_t first, uint32_t count, uint32_t depth) {
+    // leaves hold at most kMaxLeafSize triangles; larger ranges become a
+    // small subtree of full leaves (only reachable when centroids coincide)
+    if (count > (uint32_t)kMaxLeafSize) {
+      const uint32_t mid = first + count / 2;
+      const int32_t l = build(first, mid - first, depth + 1);
+      const int32_t r = build(mid, first + count - mid, depth + 1);
+      nodes[id].child[0] = l;
+      nodes[id].child[1] = r;
+      return;
+    }
+    nodes[id].first = first;
+    nodes[id].count = count;
+    max_depth = std::max(max_depth, depth);
+  }
+};
+
+inline uint32_t fbits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+inline float bitsf(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+}  // namespace
+
+bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indices, uint32_t num_triangles,
+               const BvhBuildOptions& opt, BvhResult& out, std::string& error) {
+  if (num_triangles == 0) { error = "empty scene"; return false; }
+  if (opt.max_leaf_size == 0 || opt.max_leaf_size > (uint32_t)kMaxLeafSize) { error = "bad leaf size"; return false; }
+  if (num_triangles >= (1u << (31 - kLeafCountBits))) { error = "too many triangles"; return false; }
+  Builder b(opt);
+  const size_t stride = stride_bytes / sizeof(float);
+  auto P = [&](uint32_t vi) { return positions + (size_t)vi * stride; };
+  b.prim_box.resize(num_triangles);
+  b.centroid.resize(3 * (size_t)num_triangles);
+  b.order.resize(num_triangles);
+  for (uint32_t t = 0; t < num_triangles; ++t) {
+    Box bx;
+    for (int k = 0; k < 3; ++k) bx.grow(P(indices[3 * t + k]));
+    b.prim_box[t] = bx;
+    for (int k = 0; k < 3; ++k) b.centroid[3 * t + k] = 0.5f * (bx.lo[k] + bx.hi[k]);
+    b.order[t] = t;
+  }
+  b.nodes.reserve(2 * (size_t)num_triangles / std::max<uint32_t>(1, opt.max_leaf_size) + 16);
+  b.build(0, num_triangles, 0);
+  if (!b.err.empty()) { error = b.err; return false; }
+
+  // ---- layout: BFS for the top interior nodes, DFS below -----------------
+  const std::vector<BuildNode>& bn = b.nodes;
+  std::vector<int32_t> out_index(bn.size(), -1);
+  std::vector<int32_t> emit_order;   // build ids of interior nodes in output order
+  auto is_leaf = [&](int32_t id) { return bn[id].child[0] < 0; };
+  if (!is_leaf(0)) {
+    std::deque<int32_t> q{0};
+    while (!q.empty() && emit_order.size() < opt.lds_node_budget) {
+      const int32_t id = q.front();
+      q.pop_front();
+      out_index[id] = (int32_t)emit_order.size();
+      emit_order.push_back(id);
+      for (int c = 0; c < 2; ++c)
+        if (!is_leaf(bn[id].child[c])) q.push_back(bn[id].child[c]);
+    }
+    out.lds_nodes = (uint32_t)emit_order.size();
+    // remaining frontier subtrees in DFS order
+    std::vector<int32_t> stack;
+    for (int32_t root_id : q) {
+      stack.push_back(root_id);
+      while (!stack.empty()) {
+        const int32_t id = stack.back();
+        stack.pop_back();
+        out_index[id] = (int32_t)emit_order.size();
+        emit_order.push_back(id);
+        for (int c = 1; c >= 0; --c)
+          if (!is_leaf(bn[id].child[c])) stack.push_back(bn[id].child[c]);
+      }
+    }
+  }
+  // leaf triangle runs in output order of their parents (DFS-ish locality)
+  std::vector<int32_t> leaf_ref_of(bn.size(), 0);
+  uint32_t tri_cursor = 0;
+  out.tris.assign(12 * (size_t)num_triangles, 0.0f);
+  auto emit_leaf = [&](int32_t id) {
+    const BuildNode& n = bn[id];
+    for (uint32_t i = 0; i < n.count; ++i) {
+      const uint32_t prim = b.order[n.first + i];
+      const float* v0 = P(indices[3 * prim]);
+      const float* v1 = P(indices[3 * prim + 1]);
+      const float* v2 = P(indices[3 * prim + 2]);
+      float* o = &out.tris[12 * (size_t)(tri_cursor + i)];
+      o[0] = v0[0]; o[1] = v0[1]; o[2] = v0[2]; o[3] = bitsf(prim);
+      o[4] = v1[0] - v0[0]; o[5] = v1[1] - v0[1]; o[6] = v1[2] - v0[2]; o[7] = 0.0f;
+      o[8] = v2[0] - v0[0]; o[9] = v2[1] - v0[1]; o[10] = v2[2] - v0[2]; o[11] = 0.0f;
+    }
+    leaf_ref_of[id] = leaf_ref(tri_cursor, n.count);
+    tri_cursor += n.count;
+    out.num_leaves++;
+  };
+  if (is_leaf(0)) {
+    emit_leaf(0);
+    out.root = leaf_ref_of[0];
+  } else {
+    for (int32_t id : emit_order)
+      for (int c = 0; c < 2; ++c)
+        if (is_leaf(bn[id].child[c])) emit_leaf(bn[id].child[c]);
+    out.root = 0;
+  }
+  out.num_nodes = (uint32_t)emit_order.size();
+  out.nodes.assign(16 * (size_t)std::max<uint32_t>(1, out.num_nodes), 0.0f);
+  auto padded = [](const Box& bx, float lo[3], float hi[3]) {
+    for (int k = 0; k < 3; ++k) {
+      const float m = std::max(std::fabs(bx.lo[k]), std::fabs(bx.hi[k]));
+      const float pad = 1e-5f * m + 1e-6f;
+      lo[k] = bx.lo[k] - pad;
+      hi[k] = bx.hi[k] + pad;
+    }
+  };
+  double sah = 0.0;
+  const double root_area = std::max(1e-30, (double)bn[0].box.area());
+  for (size_t k = 0; k < emit_order.size(); ++k) {
+    const BuildNode& n = bn[emit_order[k]];
+    float* o = &out.nodes[16 * k];
+    float l_lo[3], l_hi[3], r_lo[3], r_hi[3];
+    const BuildNode& L = bn[n.child[0]];
+    const BuildNode& R = bn[n.child[1]];
+    padded(L.box, l_lo, l_hi);
+    padded(R.box, r_lo, r_hi);
+    o[0] = l_lo[0]; o[1] = l_hi[0]; o[2] = l_lo[1]; o[3] = l_hi[1];
+    o[4] = r_lo[0]; o[5] = r_hi[0]; o[6] = r_lo[1]; o[7] = r_hi[1];
+    o[8] = l_lo[2]; o[9] = l_hi[2]; o[10] = r_lo[2]; o[11] = r_hi[2];
+    const int32_t lref = is_leaf(n.child[0]) ? leaf_ref_of[n.child[0]] : out_index[n.child[0]];
+    const int32_t rref = is_leaf(n.child[1]) ? leaf_ref_of[n.child[1]] : out_index[n.child[1]];
+    o[12] = bitsf((uint32_t)lref);
+    o[13] = bitsf((uint32_t)rref);
+    sah += opt.traversal_cost * n.box.area() / root_area;
+    if (is_leaf(n.child[0])) sah += (double)L.count * L.box.area() / root_area;
+    if (is_leaf(n.child[1])) sah += (double)R.count * R.box.area() / root_area;
+  }
+  (void)fbits;
+  out.sah_cost = sah;
+  out.max_depth = b.max_depth;
+  if (tri_cursor != num_triangles) { error = "internal: leaf triangle count mismatch"; return false; }
+  return true;
+}
+
+}  // namespace mrt

@@ -1,0 +1,50 @@
+// bvh.h — acceleration-structure build, the replacement for
+// MPSTriangleAccelerationStructure.rebuild (renderer/Renderer.mm:456-462).
+//
+// CPU binned-SAH BVH2 over the flattened triangles (vertex stride 24 B,
+// uint32 indices, triangleCount = indices/3 exactly as the reference feeds
+// MPS), emitted in the MI355X node layout documented in mrt_layout.h:
+//   * interior nodes carry both child boxes (one 64-B line per visit);
+//   * the first `lds_nodes` interior nodes are in breadth-first order (the
+//     top levels, staged into LDS by the traversal kernels), the rest in
+//     depth-first order (parent and nearer child share lines/pages);
+//   * leaves (<= 16 triangles) reference a contiguous run of the leaf-ordered
+//     triangle array {v0|prim, e1, e2}.
+// Boxes are padded outward so the slab test is conservative under rounding:
+// traversal then returns exactly the brute-force nearest hit.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mrt_layout.h"
+
+namespace mrt {
+
+struct BvhBuildOptions {
+  uint32_t max_leaf_size = 4;     // <= kMaxLeafSize
+  uint32_t lds_node_budget = 256; // interior nodes placed first in BFS order
+  uint32_t bins = 16;
+  float traversal_cost = 1.0f;    // relative to one triangle test
+};
+
+struct BvhResult {
+  std::vector<float> nodes;       // 16 floats per interior node
+  std::vector<float> tris;        // 12 floats per leaf-ordered triangle
+  int32_t root = 0;
+  uint32_t num_nodes = 0;
+  uint32_t num_leaves = 0;
+  uint32_t max_depth = 0;         // deepest leaf (root = 0); traversal needs <= max_depth stack entries
+  uint32_t lds_nodes = 0;         // top BFS-ordered nodes (min(budget, num_nodes))
+  double sah_cost = 0.0;
+};
+
+// positions: 3 floats per vertex at `stride_bytes` stride (24 for RefVertex).
+bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indices, uint32_t num_triangles,
+               const BvhBuildOptions& opt, BvhResult& out, std::string& error);
+
+inline int32_t leaf_ref(uint32_t first, uint32_t count) {
+  return (int32_t)~((first << kLeafCountBits) | (count - 1));
+}
+
+}  // namespace mrt

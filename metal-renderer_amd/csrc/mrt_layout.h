@@ -1,0 +1,94 @@
+// mrt_layout.h — data layouts shared by the host orchestration (C++) and the
+// gfx950 kernels (HIP).  Plain structs of plain pointers; no torch types.
+//
+// Two families of layouts live here:
+//   1. the REFERENCE AoS records (renderer/Raytracing.h:47-123), used only by
+//      the stage-level C ABI (mrt_raygen / mrt_intersect / mrt_shade / ...)
+//      so reference-layout buffers can be replayed for parity;
+//   2. the MI355X-native layouts used by the fused wavefront path:
+//        * ray queue: SoA of four float4 planes (16-B lane loads, 1 KiB per
+//          wave instruction, fully coalesced);
+//        * BVH2 nodes: 64-B records (both child boxes + child refs) so one
+//          node visit is four 16-B loads from one 64-B line;
+//        * leaf triangles: {v0|prim, e1, e2} float4 triples in leaf order;
+//        * per-primitive shading records (positions, normals, material and
+//          light ids) in primitive order so a hit gathers 6 x 16 B with no
+//          dependent index loads.
+#pragma once
+#include <stdint.h>
+
+namespace mrt {
+
+// ---- renderer/Raytracing.h:11-33 ------------------------------------------
+constexpr float kDistanceEpsilon = 0.0001f;          // DISTANCE_EPSILON
+constexpr float kAngleEpsilon = 0.00003807693583f;   // ANGLE_EPSILON
+constexpr float kPi = 3.1415926f;                    // PI (truncated, as in the reference)
+constexpr unsigned kNoiseDim = 64;                   // NOISE_DIMENSIONS
+constexpr unsigned kNoiseFloats = kNoiseDim * kNoiseDim * 4;
+constexpr unsigned kTile = 64;                       // shard tile edge (== NOISE_DIMENSIONS)
+
+// ---- renderer/Raytracing.h:35-43 ------------------------------------------
+enum MaterialType : uint32_t { kDiffuse = 0, kMirror = 1, kPlastic = 2, kDielectric = 3 };
+
+// ---- reference AoS records (renderer/Raytracing.h:47-123) -----------------
+struct RefRay {               // Ray, 80 B (vector_float4 params is 16-B aligned)
+  float origin[3]; float minDistance;
+  float direction[3]; float maxDistance;
+  float throughput[3]; float radiance[3];
+  float pad_[2];
+  float params[4];            // (material pdf, prev-is-diffuse, bounce, ior)
+};
+struct RefShadowRay {         // LightSamplingRay, 48 B
+  float origin[3]; float minDistance;
+  float direction[3]; float maxDistance;
+  float throughput[3]; uint32_t targetIndex;
+};
+struct RefIntersection { float distance; uint32_t triangleIndex; float coordinates[2]; };  // 16 B
+struct RefVertex { float v[3]; float n[3]; };                                              // 24 B
+struct RefMaterial { float diffuse[3]; float emissive[3]; float ior; uint32_t materialType; };  // 32 B
+struct RefTriangleReference { uint32_t tri[3]; uint32_t materialIndex; uint32_t lightTriangleIndex; };  // 20 B
+struct RefLightTriangle {     // 100 B
+  float emissive[3]; RefVertex v1, v2, v3; float area, pdf, cdf; uint32_t index;
+};
+static_assert(sizeof(RefRay) == 80, "RefRay");
+static_assert(sizeof(RefShadowRay) == 48, "RefShadowRay");
+static_assert(sizeof(RefIntersection) == 16, "RefIntersection");
+static_assert(sizeof(RefVertex) == 24, "RefVertex");
+static_assert(sizeof(RefMaterial) == 32, "RefMaterial");
+static_assert(sizeof(RefTriangleReference) == 20, "RefTriangleReference");
+static_assert(sizeof(RefLightTriangle) == 100, "RefLightTriangle");
+
+// ---- device scene (MI355X layout) -----------------------------------------
+// BVH2 node i = nodes[4i .. 4i+3]:
+//   [0] = (L.lo.x, L.hi.x, L.lo.y, L.hi.y)
+//   [1] = (R.lo.x, R.hi.x, R.lo.y, R.hi.y)
+//   [2] = (L.lo.z, L.hi.z, R.lo.z, R.hi.z)
+//   [3] = (bits(Lref), bits(Rref), 0, 0)
+// ref >= 0: interior node index; ref < 0: leaf, ~ref = (first << 4) | (count-1)
+constexpr int kLeafCountBits = 4;
+constexpr int kMaxLeafSize = 1 << kLeafCountBits;   // 16
+constexpr int kMaxStack = 32;                       // traversal stack entries per ray (LDS)
+constexpr int kMaxBvhDepth = kMaxStack;             // builder forces leaves below this depth
+
+// Device-resident scene, passed to kernels by value.  Every pointer is
+// 16-B aligned device memory; float pointers documented as "float4" hold
+// 4 floats per record.
+struct DeviceScene {
+  const float* nodes;        // float4 x 4 per BVH node (see above)
+  const float* tris;         // float4 x 3 per leaf-ordered triangle: (v0, bits(prim)), (e1, 0), (e2, 0)
+  const float* prims;        // float4 x 6 per primitive (original order):
+                             //   (p0, bits(material)), (p1, bits(light index or ~0u)), (p2, 0),
+                             //   (n0, 0), (n1, 0), (n2, 0)
+  const float* materials;    // float4 x 2 per material: (diffuse, ior), (emissive, bits(type))
+  const float* lights;       // float4 x 7 per light entry (incl. sentinel):
+                             //   (emissive, area), (v1.p, pdf), (v1.n, cdf), (v2.p, bits(index)),
+                             //   (v2.n, 0), (v3.p, 0), (v3.n, 0)
+  int32_t root;              // root node ref (may be a leaf ref for tiny scenes)
+  uint32_t num_nodes;
+  uint32_t num_triangles;
+  uint32_t num_materials;
+  uint32_t num_lights;       // light triangles, excluding the sentinel (SharedData.lightTrianglesCount)
+  uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
+};
+
+}  // namespace mrt

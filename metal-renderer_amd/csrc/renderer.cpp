@@ -1,0 +1,697 @@
+// renderer.cpp — host orchestration + the C ABI of include/mrt.h.
+//
+// mrt_renderer_draw_n mirrors performRaytracing: (renderer/Renderer.mm:500-585)
+// frame by frame, restructured for MI355X as a wavefront of fused bounce
+// launches (kernels.hip::bounce_kernel):
+//   reference per frame: rayGenerator, L x {MPS intersect, intersectionHandler,
+//                        MPS intersect (shadow), lightSamplingHandler},
+//                        accumulateImage                       = 2 + 4L passes
+//   here per frame:      L bounce launches over a compacted SoA ray queue
+//                        (raygen fused into bounce 0, shadow resolve and
+//                        accumulation fused into the bounce where the path
+//                        ends)                                 = L launches
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mrt.h"
+#include "bvh.h"
+#include "kernels.h"
+#include "noise.h"
+#include "scene.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess)                                                                         \
+      return fail(MRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));                \
+  } while (0)
+
+inline float bitsf(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t n) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+    bytes = n;
+    return n ? hipMalloc(&p, n) : hipSuccess;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+hipError_t upload(DevBuf& b, const void* src, size_t n) {
+  hipError_t e = b.alloc(std::max<size_t>(n, 16));
+  if (e != hipSuccess) return e;
+  return n ? hipMemcpy(b.p, src, n, hipMemcpyHostToDevice) : hipSuccess;
+}
+
+}  // namespace
+
+struct mrt_scene {
+  int device = 0;
+  mrt::HostScene host;
+  mrt::BvhResult bvh;
+  DevBuf nodes, tris, prims, materials, lights;
+  mrt::DeviceScene dev{};
+  mrt_scene_info info{};
+};
+
+struct mrt_renderer {
+  const mrt_scene* scene = nullptr;
+  mrt_renderer_desc desc{};
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  float* image = nullptr;
+  bool own_image = false;
+  uint32_t tiles_x = 0, tiles_y = 0, owned_tiles = 0;
+  uint64_t owned_pixels = 0;
+  DevBuf queue[2][4];
+  DevBuf counters;
+  // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
+  DevBuf noise_init, noise_window;
+  int64_t noise_first = 0, noise_count = 0;
+  uint64_t frame_index = 0;
+  // pending draw bookkeeping
+  bool pending = false;
+  uint32_t pending_frames = 0;
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  std::vector<hipEvent_t> kernel_events;   // MRT_FLAG_PROFILE: 2 per bounce launch
+  size_t pending_events = 0;
+  mrt_stats stats{};
+  uint32_t stack_entries = 32;
+};
+
+namespace {
+
+int finalize_pending(mrt_renderer* r) {
+  if (!r->pending) return MRT_OK;
+  HIP_TRY(hipEventSynchronize(r->ev_stop));
+  float ms = 0.0f;
+  HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
+  const uint32_t L = r->desc.max_path_length;
+  std::vector<uint32_t> cnt((size_t)r->pending_frames * L);
+  HIP_TRY(hipMemcpy(cnt.data(), r->counters.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+  uint64_t active = 0;
+  for (uint32_t f = 0; f < r->pending_frames; ++f) {
+    active += r->owned_pixels;                       // bounce 0: every owned pixel's camera ray
+    for (uint32_t b = 0; b + 1 < L; ++b) active += cnt[(size_t)f * L + b];
+  }
+  r->stats.active_ray_bounces += active;
+  r->stats.last_draw_ms = ms;
+  const uint64_t paths = r->owned_pixels * r->pending_frames;
+  r->stats.mpaths_per_s = ms > 0.0f ? (double)paths / (ms * 1e-3) / 1e6 : 0.0;
+  if (r->desc.flags & MRT_FLAG_PROFILE) {
+    for (size_t k = 0; k + 1 < r->pending_events; k += 2) {
+      float kms = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&kms, r->kernel_events[k], r->kernel_events[k + 1]));
+      r->stats.kernel_ms += kms;
+      r->stats.kernel_launches += 1;
+    }
+  }
+  r->pending = false;
+  return MRT_OK;
+}
+
+int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
+  if (!r->noise_init.p) {
+    std::vector<float> t(mrt::kNoiseFloats);
+    mrt::make_noise_table(r->desc.seed, -1, t.data());
+    HIP_TRY(upload(r->noise_init, t.data(), t.size() * 4));
+  }
+  const int64_t lo = std::max<int64_t>(0, f0 - 2), hi = f0 + (int64_t)n;   // [lo, hi)
+  if (r->noise_window.p && lo >= r->noise_first && hi <= r->noise_first + r->noise_count) return MRT_OK;
+  const int64_t count = hi - lo;
+  std::vector<float> host((size_t)count * mrt::kNoiseFloats);
+  const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int64_t k = t; k < count; k += nt)
+        mrt::make_noise_table(r->desc.seed, lo + k, host.data() + (size_t)k * mrt::kNoiseFloats);
+    });
+  for (auto& x : th) x.join();
+  if (r->pending) { int rc = finalize_pending(r); if (rc) return rc; }
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  HIP_TRY(upload(r->noise_window, host.data(), host.size() * 4));
+  r->noise_first = lo;
+  r->noise_count = count;
+  return MRT_OK;
+}
+
+const float* noise_ptr(const mrt_renderer* r, int64_t frame) {
+  if (frame < 0) return r->noise_init.as<float>();
+  return r->noise_window.as<float>() + (size_t)(frame - r->noise_first) * mrt::kNoiseFloats;
+}
+
+int alloc_frame_buffers(mrt_renderer* r) {
+  const uint32_t W = r->desc.width, H = r->desc.height;
+  const uint32_t S = std::max<uint32_t>(1, r->desc.shard_count);
+  r->tiles_x = (W + mrt::kTile - 1) / mrt::kTile;
+  r->tiles_y = (H + mrt::kTile - 1) / mrt::kTile;
+  const uint32_t T = r->tiles_x * r->tiles_y;
+  r->owned_tiles = r->desc.shard_rank < T ? (T - r->desc.shard_rank + S - 1) / S : 0;
+  r->owned_pixels = 0;
+  for (uint32_t t = r->desc.shard_rank; t < T; t += S) {
+    const uint32_t tx = t % r->tiles_x, ty = t / r->tiles_x;
+    const uint64_t w = std::min<uint32_t>(mrt::kTile, W - tx * mrt::kTile);
+    const uint64_t h = std::min<uint32_t>(mrt::kTile, H - ty * mrt::kTile);
+    r->owned_pixels += w * h;
+  }
+  const size_t slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096);
+  for (int q = 0; q < 2; ++q)
+    for (int p = 0; p < 4; ++p) HIP_TRY(r->queue[q][p].alloc(slots * 16));
+  if (r->own_image) {
+    if (r->image) (void)hipFree(r->image);
+    r->image = nullptr;
+    HIP_TRY(hipMalloc(&r->image, (size_t)W * H * 16));
+  }
+  HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)W * H * 16, r->stream));
+  r->frame_index = 0;
+  r->stats = mrt_stats{};
+  r->stats.owned_pixels = r->owned_pixels;
+  return MRT_OK;
+}
+
+inline hipError_t launch_bounce(const mrt_renderer* r, const mrt::BounceArgs& a) {
+  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_bounce(r->scene->dev, a, r->stack_entries, r->stream);
+  return mrt::fast::launch_bounce(r->scene->dev, a, r->stack_entries, r->stream);
+}
+
+bool precise(uint32_t flags) { return (flags & MRT_FLAG_PRECISE) != 0; }
+
+int write_pfm(const char* path, const std::vector<float>& rgba, uint32_t W, uint32_t H) {
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return fail(MRT_ERR_IO, std::string("cannot write ") + path);
+  std::fprintf(f, "PF\n%u %u\n-1.0\n", W, H);
+  std::vector<float> row(3 * (size_t)W);
+  for (uint32_t y = 0; y < H; ++y) {   // PFM scanlines are bottom-to-top == our row order
+    for (uint32_t x = 0; x < W; ++x)
+      for (int c = 0; c < 3; ++c) row[3 * x + c] = rgba[4 * ((size_t)y * W + x) + c];
+    std::fwrite(row.data(), 4, row.size(), f);
+  }
+  std::fclose(f);
+  return MRT_OK;
+}
+
+// Uncompressed scanline OpenEXR, FLOAT A,B,G,R channels, top-down.
+int write_exr(const char* path, const std::vector<float>& rgba, uint32_t W, uint32_t H) {
+  std::vector<uint8_t> out;
+  auto put = [&](const void* p, size_t n) { const uint8_t* b = (const uint8_t*)p; out.insert(out.end(), b, b + n); };
+  auto put_i32 = [&](int32_t v) { put(&v, 4); };
+  auto put_str = [&](const char* s) { put(s, std::strlen(s) + 1); };
+  auto attr = [&](const char* name, const char* type, const std::vector<uint8_t>& v) {
+    put_str(name); put_str(type); put_i32((int32_t)v.size()); put(v.data(), v.size());
+  };
+  const uint32_t magic = 20000630u, version = 2u;
+  put(&magic, 4); put(&version, 4);
+  std::vector<uint8_t> ch;
+  for (const char* c : {"A", "B", "G", "R"}) {
+    ch.insert(ch.end(), c, c + 2);
+    const int32_t pt = 2;  // FLOAT
+    const uint8_t plin[4] = {0, 0, 0, 0};
+    const int32_t xs = 1, ys = 1;
+    ch.insert(ch.end(), (const uint8_t*)&pt, (const uint8_t*)&pt + 4);
+    ch.insert(ch.end(), plin, plin + 4);
+    ch.insert(ch.end(), (const uint8_t*)&xs, (const uint8_t*)&xs + 4);
+    ch.insert(ch.end(), (const uint8_t*)&ys, (const uint8_t*)&ys + 4);
+  }
+  ch.push_back(0);
+  attr("channels", "chlist", ch);
+  attr("compression", "compression", {0});
+  const int32_t box[4] = {0, 0, (int32_t)W - 1, (int32_t)H - 1};
+  std::vector<uint8_t> bx((const uint8_t*)box, (const uint8_t*)box + 16);
+  attr("dataWindow", "box2i", bx);
+  attr("displayWindow", "box2i", bx);
+  attr("lineOrder", "lineOrder", {0});
+  const float par = 1.0f, ssw = 1.0f, swc[2] = {0.0f, 0.0f};
+  attr("pixelAspectRatio", "float", std::vector<uint8_t>((const uint8_t*)&par, (const uint8_t*)&par + 4));
+  attr("screenWindowCenter", "v2f", std::vector<uint8_t>((const uint8_t*)swc, (const uint8_t*)swc + 8));
+  attr("screenWindowWidth", "float", std::vector<uint8_t>((const uint8_t*)&ssw, (const uint8_t*)&ssw + 4));
+  out.push_back(0);
+  const size_t line_bytes = (size_t)W * 4 * 4;
+  uint64_t off = out.size() + 8ull * H;
+  for (uint32_t y = 0; y < H; ++y) { put(&off, 8); off += 8 + line_bytes; }
+  std::vector<float> line(4 * (size_t)W);
+  for (uint32_t y = 0; y < H; ++y) {
+    const uint32_t src = H - 1 - y;   // EXR is top-down; our row 0 is the bottom
+    for (int c = 0; c < 4; ++c) {      // A, B, G, R
+      const int comp = 3 - c;
+      for (uint32_t x = 0; x < W; ++x) line[(size_t)c * W + x] = rgba[4 * ((size_t)src * W + x) + comp];
+    }
+    put_i32((int32_t)y);
+    put_i32((int32_t)line_bytes);
+    put(line.data(), line_bytes);
+  }
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return fail(MRT_ERR_IO, std::string("cannot write ") + path);
+  std::fwrite(out.data(), 1, out.size(), f);
+  std::fclose(f);
+  return MRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mrt_last_error(void) { return g_last_error.c_str(); }
+int mrt_abi_version(void) { return MRT_ABI_VERSION; }
+
+int mrt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int mrt_noise_table(uint64_t seed, int64_t frame, float* out) {
+  if (!out) return fail(MRT_ERR_INVALID, "null output");
+  mrt::make_noise_table(seed, frame, out);
+  return MRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// scene
+// ---------------------------------------------------------------------------
+int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
+  if (!desc || !out || !desc->obj_path) return fail(MRT_ERR_INVALID, "mrt_scene_create: null argument");
+  *out = nullptr;
+  std::unique_ptr<mrt_scene> s(new mrt_scene());
+  s->device = desc->device;
+  std::string err;
+  if (!mrt::import_obj(desc->obj_path, desc->mtl_override ? desc->mtl_override : "", s->host, err))
+    return fail(MRT_ERR_IO, err);
+  if (desc->procedural_triangles) mrt::append_procedural_mesh(s->host, desc->procedural_triangles, desc->procedural_seed);
+  mrt::flatten(s->host);
+  const mrt::HostScene& h = s->host;
+  const uint32_t T = (uint32_t)h.references.size();
+
+  mrt::BvhBuildOptions opt;
+  if (desc->max_leaf_size) opt.max_leaf_size = desc->max_leaf_size;
+  if (desc->lds_nodes == UINT32_MAX) opt.lds_node_budget = 0;
+  else if (desc->lds_nodes) opt.lds_node_budget = desc->lds_nodes;
+  else opt.lds_node_budget = 128;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), h.indices.data(), T, opt, s->bvh, err))
+    return fail(MRT_ERR_INVALID, "BVH build failed: " + err);
+  const double build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (s->bvh.max_depth >= (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_INVALID, "BVH deeper than the traversal stack");
+
+  // per-primitive shading records (primitive order)
+  std::vector<float> prims((size_t)T * 24);
+  for (uint32_t t = 0; t < T; ++t) {
+    const mrt::RefTriangleReference& r = h.references[t];
+    float* o = &prims[(size_t)t * 24];
+    for (int k = 0; k < 3; ++k) {
+      const mrt::RefVertex& v = h.vertices[r.tri[k]];
+      o[4 * k + 0] = v.v[0]; o[4 * k + 1] = v.v[1]; o[4 * k + 2] = v.v[2]; o[4 * k + 3] = 0.0f;
+      o[12 + 4 * k + 0] = v.n[0]; o[12 + 4 * k + 1] = v.n[1]; o[12 + 4 * k + 2] = v.n[2]; o[12 + 4 * k + 3] = 0.0f;
+    }
+    o[3] = bitsf(r.materialIndex);
+    o[7] = bitsf(r.lightTriangleIndex);
+  }
+  std::vector<float> mats(h.materials.size() * 8);
+  for (size_t m = 0; m < h.materials.size(); ++m) {
+    const mrt::RefMaterial& M = h.materials[m];
+    float* o = &mats[m * 8];
+    o[0] = M.diffuse[0]; o[1] = M.diffuse[1]; o[2] = M.diffuse[2]; o[3] = M.ior;
+    o[4] = M.emissive[0]; o[5] = M.emissive[1]; o[6] = M.emissive[2]; o[7] = bitsf(M.materialType);
+  }
+  std::vector<float> lights(h.lights.size() * 28, 0.0f);
+  for (size_t l = 0; l < h.lights.size(); ++l) {
+    const mrt::RefLightTriangle& L = h.lights[l];
+    float* o = &lights[l * 28];
+    o[0] = L.emissive[0]; o[1] = L.emissive[1]; o[2] = L.emissive[2]; o[3] = L.area;
+    const mrt::RefVertex* v[3] = {&L.v1, &L.v2, &L.v3};
+    for (int k = 0; k < 3; ++k) {
+      for (int c = 0; c < 3; ++c) { o[4 + 8 * k + c] = v[k]->v[c]; o[8 + 8 * k + c] = v[k]->n[c]; }
+    }
+    o[7] = L.pdf;
+    o[11] = L.cdf;
+    o[15] = bitsf(L.index);
+  }
+  mrt_scene_info& in = s->info;
+  in.vertices = (uint32_t)h.vertices.size();
+  in.triangles = T;
+  in.materials = (uint32_t)h.materials.size();
+  in.light_triangles = h.light_count;
+  in.bvh_nodes = s->bvh.num_nodes;
+  in.bvh_leaves = s->bvh.num_leaves;
+  in.bvh_depth = s->bvh.max_depth;
+  in.bvh_lds_nodes = s->bvh.lds_nodes;
+  in.bvh_sah_cost = s->bvh.sah_cost;
+  in.build_ms = build_ms;
+  if (desc->device < 0) {   // host-only scene (CPU tests of import + BVH)
+    *out = s.release();
+    return MRT_OK;
+  }
+  HIP_TRY(hipSetDevice(desc->device));
+  HIP_TRY(upload(s->nodes, s->bvh.nodes.data(), s->bvh.nodes.size() * 4));
+  HIP_TRY(upload(s->tris, s->bvh.tris.data(), s->bvh.tris.size() * 4));
+  HIP_TRY(upload(s->prims, prims.data(), prims.size() * 4));
+  HIP_TRY(upload(s->materials, mats.data(), mats.size() * 4));
+  HIP_TRY(upload(s->lights, lights.data(), lights.size() * 4));
+  mrt::DeviceScene& d = s->dev;
+  d.nodes = s->nodes.as<float>();
+  d.tris = s->tris.as<float>();
+  d.prims = s->prims.as<float>();
+  d.materials = s->materials.as<float>();
+  d.lights = s->lights.as<float>();
+  d.root = s->bvh.root;
+  d.num_nodes = s->bvh.num_nodes;
+  d.num_triangles = T;
+  d.num_materials = (uint32_t)h.materials.size();
+  d.num_lights = h.light_count;
+  d.lds_nodes = s->bvh.lds_nodes;
+  in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
+  *out = s.release();
+  return MRT_OK;
+}
+
+int mrt_scene_info_get(const mrt_scene* scene, mrt_scene_info* info) {
+  if (!scene || !info) return fail(MRT_ERR_INVALID, "null argument");
+  *info = scene->info;
+  return MRT_OK;
+}
+
+int mrt_scene_export(const mrt_scene* scene, void* vertices, void* indices, void* materials, void* references,
+                     void* lights) {
+  if (!scene) return fail(MRT_ERR_INVALID, "null scene");
+  const mrt::HostScene& h = scene->host;
+  if (vertices) std::memcpy(vertices, h.vertices.data(), h.vertices.size() * sizeof(mrt::RefVertex));
+  if (indices) std::memcpy(indices, h.indices.data(), h.indices.size() * 4);
+  if (materials) std::memcpy(materials, h.materials.data(), h.materials.size() * sizeof(mrt::RefMaterial));
+  if (references) std::memcpy(references, h.references.data(), h.references.size() * sizeof(mrt::RefTriangleReference));
+  if (lights) std::memcpy(lights, h.lights.data(), h.lights.size() * sizeof(mrt::RefLightTriangle));
+  return MRT_OK;
+}
+
+int mrt_scene_check_bvh(const mrt_scene* scene) {
+  if (!scene) return fail(MRT_ERR_INVALID, "null scene");
+  const mrt::BvhResult& b = scene->bvh;
+  const mrt::HostScene& h = scene->host;
+  const uint32_t T = (uint32_t)h.references.size();
+  std::vector<uint8_t> seen(T, 0);
+  auto fbits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+  // returns false on violation; checks triangle containment in the given box
+  struct Item { int32_t ref; float lo[3], hi[3]; uint32_t depth; };
+  std::vector<Item> stack;
+  Item root{b.root, {-1e30f, -1e30f, -1e30f}, {1e30f, 1e30f, 1e30f}, 0};
+  stack.push_back(root);
+  uint32_t nodes_seen = 0;
+  while (!stack.empty()) {
+    Item it = stack.back();
+    stack.pop_back();
+    if (it.depth >= (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_STATE, "BVH too deep");
+    if (it.ref >= 0) {
+      if ((uint32_t)it.ref >= b.num_nodes) return fail(MRT_ERR_STATE, "BVH node index out of range");
+      ++nodes_seen;
+      const float* n = &b.nodes[16 * (size_t)it.ref];
+      Item l{(int32_t)fbits(n[12]), {n[0], n[2], n[8]}, {n[1], n[3], n[9]}, it.depth + 1};
+      Item r{(int32_t)fbits(n[13]), {n[4], n[6], n[10]}, {n[5], n[7], n[11]}, it.depth + 1};
+      for (int k = 0; k < 3; ++k)
+        if (!(l.lo[k] <= l.hi[k]) || !(r.lo[k] <= r.hi[k])) return fail(MRT_ERR_STATE, "BVH empty child box");
+      stack.push_back(l);
+      stack.push_back(r);
+    } else {
+      const uint32_t leaf = ~(uint32_t)it.ref;
+      const uint32_t first = leaf >> mrt::kLeafCountBits, cnt = (leaf & (mrt::kMaxLeafSize - 1)) + 1;
+      if (first + cnt > T) return fail(MRT_ERR_STATE, "BVH leaf range out of bounds");
+      for (uint32_t k = first; k < first + cnt; ++k) {
+        const float* t = &b.tris[12 * (size_t)k];
+        const uint32_t prim = fbits(t[3]);
+        if (prim >= T || seen[prim]) return fail(MRT_ERR_STATE, "BVH primitive missing or duplicated");
+        seen[prim] = 1;
+        for (int c = 0; c < 3; ++c) {
+          const float* p = h.vertices[h.references[prim].tri[c]].v;
+          for (int a = 0; a < 3; ++a)
+            if (!(p[a] >= it.lo[a] && p[a] <= it.hi[a])) return fail(MRT_ERR_STATE, "BVH box does not contain its triangle");
+        }
+        // leaf record = (v0, prim), (v1 - v0), (v2 - v0)
+        const float* v0 = h.vertices[h.references[prim].tri[0]].v;
+        const float* v1 = h.vertices[h.references[prim].tri[1]].v;
+        const float* v2 = h.vertices[h.references[prim].tri[2]].v;
+        for (int a = 0; a < 3; ++a)
+          if (t[a] != v0[a] || t[4 + a] != v1[a] - v0[a] || t[8 + a] != v2[a] - v0[a])
+            return fail(MRT_ERR_STATE, "BVH leaf triangle record mismatch");
+      }
+    }
+  }
+  for (uint32_t t = 0; t < T; ++t)
+    if (!seen[t]) return fail(MRT_ERR_STATE, "BVH primitive not referenced");
+  if (nodes_seen != b.num_nodes) return fail(MRT_ERR_STATE, "BVH has unreachable nodes");
+  return MRT_OK;
+}
+
+int mrt_scene_destroy(mrt_scene* scene) {
+  delete scene;
+  return MRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// stage-level ABI
+// ---------------------------------------------------------------------------
+#define STAGE_CALL(call) \
+  HIP_TRY(precise(flags) ? mrt::precise::call : mrt::fast::call)
+
+int mrt_raygen(const mrt_scene* scene, uint32_t W, uint32_t H, const float* noise, void* rays, uint32_t flags,
+               void* stream) {
+  if (!scene || !noise || !rays || W < 2 || H < 2) return fail(MRT_ERR_INVALID, "mrt_raygen: bad argument");
+  STAGE_CALL(launch_raygen(W, H, noise, (mrt::RefRay*)rays, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+int mrt_intersect(const mrt_scene* scene, const void* rays, uint32_t stride, uint32_t count, void* isect,
+                  uint32_t flags, void* stream) {
+  if (!scene || (!rays && count) || (!isect && count) || stride < 32 || (stride % 4))
+    return fail(MRT_ERR_INVALID, "mrt_intersect: bad argument");
+  STAGE_CALL(launch_intersect(scene->dev, rays, stride, count, (mrt::RefIntersection*)isect, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+int mrt_shade(const mrt_scene* scene, uint32_t W, uint32_t H, uint32_t frame_index, uint32_t L, const float* noise,
+              const void* isect, void* rays, void* srays, uint32_t flags, void* stream) {
+  if (!scene || !noise || !isect || !rays || !srays || W == 0 || H == 0 || L == 0)
+    return fail(MRT_ERR_INVALID, "mrt_shade: bad argument");
+  STAGE_CALL(launch_shade(scene->dev, W, H, frame_index, L, noise, (const mrt::RefIntersection*)isect,
+                          (mrt::RefRay*)rays, (mrt::RefShadowRay*)srays, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+int mrt_resolve_shadow(const mrt_scene* scene, uint32_t count, const void* isect, void* rays, const void* srays,
+                       uint32_t flags, void* stream) {
+  if (!scene || (count && (!isect || !rays || !srays))) return fail(MRT_ERR_INVALID, "mrt_resolve_shadow: bad argument");
+  STAGE_CALL(launch_resolve(count, (const mrt::RefIntersection*)isect, (mrt::RefRay*)rays,
+                            (const mrt::RefShadowRay*)srays, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+int mrt_accumulate(const mrt_scene* scene, uint32_t W, uint32_t H, uint32_t frame_index, const void* rays,
+                   float* image, uint32_t flags, void* stream) {
+  if (!scene || !rays || !image || W == 0 || H == 0) return fail(MRT_ERR_INVALID, "mrt_accumulate: bad argument");
+  STAGE_CALL(launch_accumulate(W, H, frame_index, (const mrt::RefRay*)rays, image, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// renderer
+// ---------------------------------------------------------------------------
+int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
+  if (!desc || !out || !desc->scene) return fail(MRT_ERR_INVALID, "mrt_renderer_create: null argument");
+  *out = nullptr;
+  if (desc->width < 2 || desc->height < 2 || desc->width > 32768 || desc->height > 32768)
+    return fail(MRT_ERR_INVALID, "image size must be in [2, 32768]");
+  if ((uint64_t)desc->width * desc->height >= (1ull << 31)) return fail(MRT_ERR_INVALID, "image too large");
+  if (desc->max_path_length == 0 || desc->max_path_length > 64)
+    return fail(MRT_ERR_INVALID, "max_path_length must be in [1, 64]");
+  const uint32_t S = std::max<uint32_t>(1, desc->shard_count);
+  if (desc->shard_rank >= S) return fail(MRT_ERR_INVALID, "shard_rank >= shard_count");
+  std::unique_ptr<mrt_renderer> r(new mrt_renderer());
+  r->scene = desc->scene;
+  r->desc = *desc;
+  r->desc.shard_count = S;
+  HIP_TRY(hipSetDevice(desc->scene->device));
+  if (desc->stream) {
+    r->stream = (hipStream_t)desc->stream;
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    r->own_stream = true;
+  }
+  r->own_image = desc->image == nullptr;
+  r->image = desc->image;
+  HIP_TRY(hipEventCreate(&r->ev_start));
+  HIP_TRY(hipEventCreate(&r->ev_stop));
+  const uint32_t depth = desc->scene->bvh.max_depth;
+  r->stack_entries = depth <= 8 ? 8 : depth <= 16 ? 16 : depth <= 24 ? 24 : 32;
+  int rc = alloc_frame_buffers(r.get());
+  if (rc) return rc;
+  *out = r.release();
+  return MRT_OK;
+}
+
+int mrt_renderer_resize(mrt_renderer* r, uint32_t width, uint32_t height) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  if (width < 2 || height < 2 || width > 32768 || height > 32768) return fail(MRT_ERR_INVALID, "bad size");
+  if (!r->own_image) return fail(MRT_ERR_STATE, "cannot resize an externally owned image");
+  int rc = finalize_pending(r);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  r->desc.width = width;
+  r->desc.height = height;
+  return alloc_frame_buffers(r);
+}
+
+int mrt_renderer_reset(mrt_renderer* r) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  int rc = finalize_pending(r);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)r->desc.width * r->desc.height * 16, r->stream));
+  r->frame_index = 0;
+  const uint64_t owned = r->owned_pixels;
+  r->stats = mrt_stats{};
+  r->stats.owned_pixels = owned;
+  return MRT_OK;
+}
+
+int mrt_renderer_prepare(mrt_renderer* r, uint32_t n) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  return ensure_noise(r, (int64_t)r->frame_index, std::max<uint32_t>(1, n));
+}
+
+int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  if (n == 0) return MRT_OK;
+  int rc = finalize_pending(r);
+  if (rc) return rc;
+  rc = ensure_noise(r, (int64_t)r->frame_index, n);
+  if (rc) return rc;
+  const uint32_t L = r->desc.max_path_length;
+  const size_t counter_bytes = (size_t)n * L * 4;
+  if (r->counters.bytes < counter_bytes) HIP_TRY(r->counters.alloc(counter_bytes));
+  HIP_TRY(hipMemsetAsync(r->counters.p, 0, counter_bytes, r->stream));
+  const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
+  if (profile) {
+    const size_t need = (size_t)2 * n * L;
+    while (r->kernel_events.size() < need) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      r->kernel_events.push_back(e);
+    }
+  }
+  HIP_TRY(hipEventRecord(r->ev_start, r->stream));
+  uint32_t* cnt = r->counters.as<uint32_t>();
+  size_t ev = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint64_t f = r->frame_index + k;
+    for (uint32_t b = 0; b < L; ++b) {
+      mrt::BounceArgs a{};
+      a.width = r->desc.width;
+      a.height = r->desc.height;
+      a.frame_index = (uint32_t)f;
+      a.bounce = b;
+      a.max_path_length = L;
+      a.shard_rank = r->desc.shard_rank;
+      a.shard_count = r->desc.shard_count;
+      a.tiles_x = r->tiles_x;
+      a.num_slots = r->owned_tiles * 4096u;
+      a.in_count = b ? cnt + (size_t)k * L + (b - 1) : nullptr;
+      a.out_count = cnt + (size_t)k * L + b;
+      for (int p = 0; p < 4; ++p) {
+        a.in_q.plane[p] = r->queue[b & 1][p].as<float4>();
+        a.out_q.plane[p] = r->queue[(b + 1) & 1][p].as<float4>();
+      }
+      a.noise_raygen = reinterpret_cast<const float4*>(noise_ptr(r, (int64_t)f));
+      a.noise_shade = reinterpret_cast<const float4*>(noise_ptr(r, mrt::noise_frame_for_iteration((int64_t)f, b)));
+      a.image = reinterpret_cast<float4*>(r->image);
+      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], r->stream));
+      HIP_TRY(launch_bounce(r, a));
+      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], r->stream));
+    }
+  }
+  HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
+  r->pending = true;
+  r->pending_frames = n;
+  r->pending_events = ev;
+  r->frame_index += n;
+  r->stats.frame_index = r->frame_index;
+  r->stats.paths += r->owned_pixels * n;
+  return MRT_OK;
+}
+
+int mrt_renderer_draw(mrt_renderer* r) { return mrt_renderer_draw_n(r, 1); }
+
+int mrt_renderer_sync(mrt_renderer* r) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  int rc = finalize_pending(r);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  return MRT_OK;
+}
+
+int mrt_renderer_image(mrt_renderer* r, float** device_image) {
+  if (!r || !device_image) return fail(MRT_ERR_INVALID, "null argument");
+  *device_image = r->image;
+  return MRT_OK;
+}
+
+int mrt_renderer_read_image(mrt_renderer* r, float* rgba, size_t count) {
+  if (!r || !rgba) return fail(MRT_ERR_INVALID, "null argument");
+  const size_t need = (size_t)r->desc.width * r->desc.height * 4;
+  if (count < need) return fail(MRT_ERR_INVALID, "output buffer too small");
+  int rc = mrt_renderer_sync(r);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(rgba, r->image, need * 4, hipMemcpyDeviceToHost));
+  return MRT_OK;
+}
+
+int mrt_renderer_save_image(mrt_renderer* r, const char* path) {
+  if (!r || !path) return fail(MRT_ERR_INVALID, "null argument");
+  const uint32_t W = r->desc.width, H = r->desc.height;
+  std::vector<float> img((size_t)W * H * 4);
+  int rc = mrt_renderer_read_image(r, img.data(), img.size());
+  if (rc) return rc;
+  const std::string p(path);
+  auto ends = [&](const char* s) { const size_t n = std::strlen(s); return p.size() >= n && p.compare(p.size() - n, n, s) == 0; };
+  if (ends(".pfm")) return write_pfm(path, img, W, H);
+  if (ends(".exr")) return write_exr(path, img, W, H);
+  return fail(MRT_ERR_INVALID, "unsupported image extension (use .pfm or .exr)");
+}
+
+int mrt_renderer_stats(const mrt_renderer* r, mrt_stats* stats) {
+  if (!r || !stats) return fail(MRT_ERR_INVALID, "null argument");
+  int rc = finalize_pending(const_cast<mrt_renderer*>(r));
+  if (rc) return rc;
+  *stats = r->stats;
+  return MRT_OK;
+}
+
+int mrt_renderer_destroy(mrt_renderer* r) {
+  if (!r) return MRT_OK;
+  (void)finalize_pending(r);
+  if (r->stream) (void)hipStreamSynchronize(r->stream);
+  if (r->own_image && r->image) (void)hipFree(r->image);
+  for (hipEvent_t e : r->kernel_events) (void)hipEventDestroy(e);
+  if (r->ev_start) (void)hipEventDestroy(r->ev_start);
+  if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
+  if (r->own_stream) (void)hipStreamDestroy(r->stream);
+  delete r;
+  return MRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,316 @@
+"""Python mirror of the reference's Renderer interface over libmrt.so (C ABI).
+
+The reference API (renderer/Renderer.h:3-8, Renderer.mm) maps to:
+
+    -initWithMetalKitView:            -> Renderer(scene, width, height, ...)
+    -mtkView:drawableSizeWillChange:  -> Renderer.resize(width, height)
+    -drawInMTKView:                   -> Renderer.draw()          (1 spp frame)
+    -saveCurrentImage                 -> Renderer.save_current_image(path)
+    title-bar "Mrays/s, ms/frame"     -> Renderer.stats()
+
+and the per-stage dispatches of performRaytracing: (Renderer.mm:500-585) map to
+the module functions raygen / intersect / shade / resolve_shadow / accumulate,
+which take device pointers (ints) to reference-layout AoS buffers.
+
+This module only binds the native library: every call runs the HIP kernels in
+libmrt.so.  There is no CPU fallback; if the library is missing the import
+fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmrt.so")
+INCLUDE_H = os.path.join(os.path.dirname(HERE), "include", "mrt.h")
+SCENES_DIR = os.path.join(os.path.dirname(HERE), "tests", "golden", "scenes")
+
+FLAG_PRECISE = 1
+FLAG_PROFILE = 2
+DEFAULT_SEED = 0x6D6574616C2D7274  # "metal-rt"
+
+RAY_BYTES, SHADOW_RAY_BYTES, ISECT_BYTES = 80, 48, 16
+
+
+class MrtError(RuntimeError):
+    pass
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [
+        ("obj_path", ctypes.c_char_p),
+        ("mtl_override", ctypes.c_char_p),
+        ("procedural_triangles", ctypes.c_uint32),
+        ("procedural_seed", ctypes.c_uint64),
+        ("max_leaf_size", ctypes.c_uint32),
+        ("lds_nodes", ctypes.c_uint32),
+        ("device", ctypes.c_int),
+    ]
+
+
+class SceneInfo(ctypes.Structure):
+    _fields_ = [
+        ("vertices", ctypes.c_uint32), ("triangles", ctypes.c_uint32), ("materials", ctypes.c_uint32),
+        ("light_triangles", ctypes.c_uint32), ("bvh_nodes", ctypes.c_uint32), ("bvh_leaves", ctypes.c_uint32),
+        ("bvh_depth", ctypes.c_uint32), ("bvh_lds_nodes", ctypes.c_uint32), ("bvh_sah_cost", ctypes.c_double),
+        ("build_ms", ctypes.c_double), ("device_bytes", ctypes.c_uint64),
+    ]
+
+
+class RendererDesc(ctypes.Structure):
+    _fields_ = [
+        ("scene", ctypes.c_void_p),
+        ("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+        ("max_path_length", ctypes.c_uint32),
+        ("seed", ctypes.c_uint64),
+        ("shard_rank", ctypes.c_uint32), ("shard_count", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("stream", ctypes.c_void_p),
+        ("image", ctypes.c_void_p),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("frame_index", ctypes.c_uint64), ("paths", ctypes.c_uint64), ("active_ray_bounces", ctypes.c_uint64),
+        ("last_draw_ms", ctypes.c_double), ("mpaths_per_s", ctypes.c_double),
+        ("kernel_launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("owned_pixels", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+EXPORTED = [
+    "mrt_scene_create", "mrt_scene_info_get", "mrt_scene_export", "mrt_scene_destroy", "mrt_scene_check_bvh",
+    "mrt_raygen", "mrt_intersect", "mrt_shade", "mrt_resolve_shadow", "mrt_accumulate",
+    "mrt_renderer_create", "mrt_renderer_resize", "mrt_renderer_reset", "mrt_renderer_prepare",
+    "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image",
+    "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
+    "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count",
+]
+
+_lib = None
+
+
+def build(jobs: int = 4) -> None:
+    """Compile libmrt.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MrtError(f"native library missing: {LIB_PATH} (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i64, c_int = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int
+    sig = {
+        "mrt_scene_create": [ctypes.POINTER(SceneDesc), ctypes.POINTER(vp)],
+        "mrt_scene_info_get": [vp, ctypes.POINTER(SceneInfo)],
+        "mrt_scene_export": [vp, vp, vp, vp, vp, vp],
+        "mrt_scene_destroy": [vp],
+        "mrt_scene_check_bvh": [vp],
+        "mrt_raygen": [vp, u32, u32, vp, vp, u32, vp],
+        "mrt_intersect": [vp, vp, u32, u32, vp, u32, vp],
+        "mrt_shade": [vp, u32, u32, u32, u32, vp, vp, vp, vp, u32, vp],
+        "mrt_resolve_shadow": [vp, u32, vp, vp, vp, u32, vp],
+        "mrt_accumulate": [vp, u32, u32, u32, vp, vp, u32, vp],
+        "mrt_renderer_create": [ctypes.POINTER(RendererDesc), ctypes.POINTER(vp)],
+        "mrt_renderer_resize": [vp, u32, u32],
+        "mrt_renderer_reset": [vp],
+        "mrt_renderer_prepare": [vp, u32],
+        "mrt_renderer_draw": [vp],
+        "mrt_renderer_draw_n": [vp, u32],
+        "mrt_renderer_sync": [vp],
+        "mrt_renderer_image": [vp, ctypes.POINTER(vp)],
+        "mrt_renderer_read_image": [vp, vp, ctypes.c_size_t],
+        "mrt_renderer_save_image": [vp, ctypes.c_char_p],
+        "mrt_renderer_stats": [vp, ctypes.POINTER(Stats)],
+        "mrt_renderer_destroy": [vp],
+        "mrt_last_error": [],
+        "mrt_abi_version": [],
+        "mrt_noise_table": [u64, i64, vp],
+        "mrt_device_count": [],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = c_int
+    L.mrt_last_error.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise MrtError(f"{what} failed ({rc}): {lib().mrt_last_error().decode()}")
+
+
+def scene_path(name: str) -> str:
+    """Path of a scene shipped under tests/golden/scenes (renderer/Media data)."""
+    return name if os.path.sep in name else os.path.join(SCENES_DIR, name if name.endswith(".obj") else name + ".obj")
+
+
+class Scene:
+    """Flattened scene + BVH on the device (initRaytracing, Renderer.mm:255-470)."""
+
+    def __init__(self, obj: str, mtl_override: str | None = None, *, procedural_triangles: int = 0,
+                 procedural_seed: int = 1, max_leaf_size: int = 0, lds_nodes: int = 0, device: int = 0):
+        self._h = None
+        d = SceneDesc(scene_path(obj).encode(), (mtl_override or "").encode(), procedural_triangles,
+                      procedural_seed, max_leaf_size, lds_nodes, device)
+        h = ctypes.c_void_p()
+        _check(lib().mrt_scene_create(ctypes.byref(d), ctypes.byref(h)), "mrt_scene_create")
+        self._h = h
+        info = SceneInfo()
+        _check(lib().mrt_scene_info_get(h, ctypes.byref(info)), "mrt_scene_info_get")
+        self.info = {k: getattr(info, k) for k, _ in SceneInfo._fields_}
+
+    @property
+    def handle(self):
+        return self._h
+
+    def export(self):
+        """Flattened reference-layout buffers as numpy structured arrays."""
+        import numpy as np
+        n = self.info
+        vt = np.dtype({"names": ["v", "n"], "formats": [("<f4", 3), ("<f4", 3)], "offsets": [0, 12], "itemsize": 24})
+        mt = np.dtype({"names": ["diffuse", "emissive", "ior", "materialType"],
+                       "formats": [("<f4", 3), ("<f4", 3), "<f4", "<u4"], "offsets": [0, 12, 24, 28], "itemsize": 32})
+        rt = np.dtype({"names": ["tri", "materialIndex", "lightTriangleIndex"],
+                       "formats": [("<u4", 3), "<u4", "<u4"], "offsets": [0, 12, 16], "itemsize": 20})
+        lt = np.dtype({"names": ["emissive", "v1", "v2", "v3", "area", "pdf", "cdf", "index"],
+                       "formats": [("<f4", 3), vt, vt, vt, "<f4", "<f4", "<f4", "<u4"],
+                       "offsets": [0, 12, 36, 60, 84, 88, 92, 96], "itemsize": 100})
+        V = np.zeros(n["vertices"], vt)
+        I = np.zeros(3 * n["triangles"], np.uint32)
+        M = np.zeros(n["materials"], mt)
+        R = np.zeros(n["triangles"], rt)
+        Lt = np.zeros(n["light_triangles"] + 1, lt)
+        p = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(lib().mrt_scene_export(self._h, p(V), p(I), p(M), p(R), p(Lt)), "mrt_scene_export")
+        return {"vertices": V, "indices": I, "materials": M, "references": R, "lights": Lt}
+
+    def check_bvh(self) -> None:
+        _check(lib().mrt_scene_check_bvh(self._h), "mrt_scene_check_bvh")
+
+    def close(self):
+        if self._h:
+            lib().mrt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Renderer:
+    """One accumulating renderer on one device (the reference's `Renderer`)."""
+
+    def __init__(self, scene: Scene, width: int, height: int, max_path_length: int = 8, *,
+                 seed: int = DEFAULT_SEED, shard_rank: int = 0, shard_count: int = 1, precise: bool = False,
+                 profile: bool = False, stream: int | None = None, image_ptr: int | None = None):
+        self._h = None
+        self.scene = scene  # keep alive
+        flags = (FLAG_PRECISE if precise else 0) | (FLAG_PROFILE if profile else 0)
+        d = RendererDesc(scene.handle, width, height, max_path_length, seed, shard_rank, shard_count, flags,
+                         stream, image_ptr)
+        h = ctypes.c_void_p()
+        _check(lib().mrt_renderer_create(ctypes.byref(d), ctypes.byref(h)), "mrt_renderer_create")
+        self._h = h
+        self.width, self.height = width, height
+
+    # -mtkView:drawableSizeWillChange:
+    def resize(self, width: int, height: int) -> None:
+        _check(lib().mrt_renderer_resize(self._h, width, height), "mrt_renderer_resize")
+        self.width, self.height = width, height
+
+    def reset(self) -> None:
+        _check(lib().mrt_renderer_reset(self._h), "mrt_renderer_reset")
+
+    def prepare(self, frames: int) -> None:
+        _check(lib().mrt_renderer_prepare(self._h, frames), "mrt_renderer_prepare")
+
+    # -drawInMTKView:
+    def draw(self, frames: int = 1) -> None:
+        _check(lib().mrt_renderer_draw_n(self._h, frames), "mrt_renderer_draw_n")
+
+    def sync(self) -> None:
+        _check(lib().mrt_renderer_sync(self._h), "mrt_renderer_sync")
+
+    def image_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        _check(lib().mrt_renderer_image(self._h, ctypes.byref(p)), "mrt_renderer_image")
+        return p.value
+
+    def read_image(self):
+        """[H, W, 4] float32, row 0 = bottom (the reference texture orientation)."""
+        import numpy as np
+        img = np.zeros((self.height, self.width, 4), np.float32)
+        _check(lib().mrt_renderer_read_image(self._h, ctypes.c_void_p(img.ctypes.data), img.size),
+               "mrt_renderer_read_image")
+        return img
+
+    # -saveCurrentImage
+    def save_current_image(self, path: str) -> None:
+        _check(lib().mrt_renderer_save_image(self._h, path.encode()), "mrt_renderer_save_image")
+
+    def stats(self) -> dict:
+        s = Stats()
+        _check(lib().mrt_renderer_stats(self._h, ctypes.byref(s)), "mrt_renderer_stats")
+        return s.as_dict()
+
+    def close(self):
+        if self._h:
+            lib().mrt_renderer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- stage-level ABI (device pointers, reference AoS layouts) -------------
+def raygen(scene: Scene, width: int, height: int, noise_ptr: int, rays_ptr: int, precise=True, stream=None):
+    _check(lib().mrt_raygen(scene.handle, width, height, noise_ptr, rays_ptr, FLAG_PRECISE if precise else 0, stream),
+           "mrt_raygen")
+
+
+def intersect(scene: Scene, rays_ptr: int, stride: int, count: int, isect_ptr: int, precise=True, stream=None):
+    _check(lib().mrt_intersect(scene.handle, rays_ptr, stride, count, isect_ptr, FLAG_PRECISE if precise else 0,
+                               stream), "mrt_intersect")
+
+
+def shade(scene: Scene, width, height, frame_index, max_path_length, noise_ptr, isect_ptr, rays_ptr, srays_ptr,
+          precise=True, stream=None):
+    _check(lib().mrt_shade(scene.handle, width, height, frame_index, max_path_length, noise_ptr, isect_ptr, rays_ptr,
+                           srays_ptr, FLAG_PRECISE if precise else 0, stream), "mrt_shade")
+
+
+def resolve_shadow(scene: Scene, count, isect_ptr, rays_ptr, srays_ptr, precise=True, stream=None):
+    _check(lib().mrt_resolve_shadow(scene.handle, count, isect_ptr, rays_ptr, srays_ptr,
+                                    FLAG_PRECISE if precise else 0, stream), "mrt_resolve_shadow")
+
+
+def accumulate(scene: Scene, width, height, frame_index, rays_ptr, image_ptr, precise=True, stream=None):
+    _check(lib().mrt_accumulate(scene.handle, width, height, frame_index, rays_ptr, image_ptr,
+                                FLAG_PRECISE if precise else 0, stream), "mrt_accumulate")
+
+
+def noise_table(seed: int, frame: int):
+    import numpy as np
+    out = np.zeros(64 * 64 * 4, np.float32)
+    _check(lib().mrt_noise_table(seed, frame, ctypes.c_void_p(out.ctypes.data)), "mrt_noise_table")
+    return out
+
+
+def device_count() -> int:
+    return int(lib().mrt_device_count())

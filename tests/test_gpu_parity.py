@@ -1,0 +1,216 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Precise build (MRT_FLAG_PRECISE): IEEE binary32, no FMA contraction, sin/cos
+correctly rounded — expected to match the oracle bit for bit; the gate is the
+BASELINE.md parity criterion (per-pixel relative L2 <= 1e-4 on >= 99.9 % of
+pixels, whole-image relative RMSE <= 1e-3), stage buffers byte-identical on
+>= 99.9 % of records.  Fast build: per-pixel relative L2 <= 1e-2 on >= 99 %.
+"""
+import numpy as np
+import pytest
+
+from helpers import SEED, dev_ptr, from_dev, pixel_metrics, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(mrt_mod, name, cache={}):
+    if name not in cache:
+        cache[name] = mrt_mod.Scene(name)
+    return cache[name]
+
+
+def _oscene(oracle_mod, mrt_mod, name, cache={}):
+    if name not in cache:
+        cache[name] = oracle_mod.OracleScene(mrt_mod.scene_path(name))
+    return cache[name]
+
+
+@pytest.mark.parametrize("W,H", [(64, 48), (257, 131)])
+def test_raygen_bitexact(gpu, mrt_mod, oracle_mod, W, H):
+    sc = _scene(mrt_mod, "cornellbox")
+    noise = oracle_mod.noise_table(SEED, 3)
+    ref = oracle_mod.raygen(W, H, noise)
+    d_noise = to_dev(noise)
+    d_rays = to_dev(np.zeros(W * H, oracle_mod.RAY_DTYPE))
+    mrt_mod.raygen(sc, W, H, dev_ptr(d_noise), dev_ptr(d_rays), precise=True)
+    got = from_dev(d_rays, oracle_mod.RAY_DTYPE)
+    assert got.tobytes() == ref.tobytes()
+
+
+def _random_rays(oracle_mod, n, rng):
+    r = np.zeros(n, oracle_mod.RAY_DTYPE)
+    r["origin"] = rng.uniform([-0.95, 0.05, -0.95], [0.95, 1.95, 2.3], size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r["direction"] = d.astype(np.float32)
+    r["maxDistance"] = np.float32(np.inf)
+    r["maxDistance"][::17] = -1.0                       # disabled rays
+    r["maxDistance"][5::23] = rng.uniform(0.01, 1.0, size=len(r["maxDistance"][5::23]))
+    # axis-aligned directions (zero components) and rays starting on surfaces
+    r["direction"][1::31] = np.array([0.0, 1.0, 0.0], np.float32)
+    r["direction"][2::31] = np.array([0.0, 0.0, -1.0], np.float32)
+    r["origin"][3::37, 1] = 0.0
+    return r
+
+
+@pytest.mark.parametrize("scene", ["cornellbox", "white-box", "CornellBox-Water-plastic"])
+@pytest.mark.parametrize("precise", [True, False])
+def test_intersect_matches_bruteforce(gpu, mrt_mod, oracle_mod, scene, precise):
+    """BVH traversal == brute-force MPS nearest-hit semantics (t, primitive, u, v)."""
+    sc, osc = _scene(mrt_mod, scene), _oscene(oracle_mod, mrt_mod, scene)
+    rng = np.random.default_rng(7)
+    rays = np.concatenate([_random_rays(oracle_mod, 6000, rng),
+                           oracle_mod.raygen(80, 60, oracle_mod.noise_table(SEED, 0))])
+    ref = osc.intersect(rays)
+    d_rays = to_dev(rays)
+    d_out = to_dev(np.zeros(len(rays), oracle_mod.ISECT_DTYPE))
+    mrt_mod.intersect(sc, dev_ptr(d_rays), 80, len(rays), dev_ptr(d_out), precise=precise)
+    got = from_dev(d_out, oracle_mod.ISECT_DTYPE)
+    hit_ref, hit_got = ref["distance"] >= 0, got["distance"] >= 0
+    if precise:
+        same = got.tobytes() == ref.tobytes()
+        mism = np.nonzero(got.view(np.uint8).reshape(-1, 16).any(1) != ref.view(np.uint8).reshape(-1, 16).any(1))
+        assert same, f"{(got != ref).sum()} mismatching intersections {mism}"
+    else:
+        agree = (hit_ref == hit_got) & (~hit_ref | (got["triangleIndex"] == ref["triangleIndex"]))
+        assert agree.mean() >= 0.999
+        both = hit_ref & hit_got & agree
+        np.testing.assert_allclose(got["distance"][both], ref["distance"][both], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("scene,L", [("cornellbox", 8), ("cornellbox", 2), ("CornellBox-Water-plastic", 8)])
+def test_stage_pipeline_bitexact(gpu, mrt_mod, oracle_mod, scene, L):
+    """One frame through the stage ABI (raygen, L x {intersect, shade, intersect,
+    resolve}, accumulate) in lockstep with the oracle's stages — the
+    reference's own dispatch order (renderer/Renderer.mm:500-585)."""
+    W, H = 48, 40
+    sc, osc = _scene(mrt_mod, scene), _oscene(oracle_mod, mrt_mod, scene)
+    f = 4
+    n_rg = oracle_mod.noise_table(SEED, f)
+    rays = oracle_mod.raygen(W, H, n_rg)
+    srays = np.zeros(W * H, oracle_mod.SRAY_DTYPE)
+    img = np.zeros((H, W, 4), np.float32)
+    d_rays = to_dev(rays)
+    d_srays = to_dev(srays)
+    d_isect = to_dev(np.zeros(W * H, oracle_mod.ISECT_DTYPE))
+    d_img = to_dev(img)
+    for i in range(L):
+        noise = oracle_mod.noise_table(SEED, oracle_mod.noise_frame_for(f, i))
+        d_noise = to_dev(noise)
+        is_ref = osc.intersect(rays)
+        mrt_mod.intersect(sc, dev_ptr(d_rays), 80, W * H, dev_ptr(d_isect))
+        assert from_dev(d_isect, oracle_mod.ISECT_DTYPE).tobytes() == is_ref.tobytes(), f"path intersect {i}"
+        osc.shade(W, H, f, L, noise, is_ref, rays, srays)
+        mrt_mod.shade(sc, W, H, f, L, dev_ptr(d_noise), dev_ptr(d_isect), dev_ptr(d_rays), dev_ptr(d_srays))
+        g_rays, g_srays = from_dev(d_rays, oracle_mod.RAY_DTYPE), from_dev(d_srays, oracle_mod.SRAY_DTYPE)
+        rec_same = (g_rays.view(np.uint8).reshape(-1, 80) == rays.view(np.uint8).reshape(-1, 80)).all(1)
+        assert rec_same.mean() >= 0.999, f"shade {i}: {np.count_nonzero(~rec_same)} ray records differ"
+        assert g_srays.tobytes() == srays.tobytes() or \
+            (g_srays.view(np.uint8).reshape(-1, 48) == srays.view(np.uint8).reshape(-1, 48)).all(1).mean() >= 0.999
+        # continue from the oracle's state so a rare flip cannot cascade
+        d_rays.copy_(to_dev(rays))
+        d_srays.copy_(to_dev(srays))
+        is2 = osc.intersect(srays)
+        mrt_mod.intersect(sc, dev_ptr(d_srays), 48, W * H, dev_ptr(d_isect))
+        assert from_dev(d_isect, oracle_mod.ISECT_DTYPE).tobytes() == is2.tobytes(), f"shadow intersect {i}"
+        oracle_mod.resolve(is2, rays, srays)
+        mrt_mod.resolve_shadow(sc, W * H, dev_ptr(d_isect), dev_ptr(d_rays), dev_ptr(d_srays))
+        assert from_dev(d_rays, oracle_mod.RAY_DTYPE).tobytes() == rays.tobytes(), f"resolve {i}"
+    oracle_mod.accumulate(0, rays, img)
+    mrt_mod.accumulate(sc, W, H, 0, dev_ptr(d_rays), dev_ptr(d_img))
+    assert from_dev(d_img, np.float32).tobytes() == img.tobytes()
+
+
+def _render_gpu(mrt_mod, sc, W, H, L, frames, precise, shard=(0, 1), seed=SEED):
+    r = mrt_mod.Renderer(sc, W, H, L, seed=seed, precise=precise, shard_rank=shard[0], shard_count=shard[1])
+    r.draw(frames)
+    img = r.read_image()
+    st = r.stats()
+    r.close()
+    return img, st
+
+
+@pytest.mark.parametrize("scene,W,H,L,frames", [
+    ("cornellbox", 64, 64, 1, 2),
+    ("cornellbox", 64, 64, 2, 3),
+    ("cornellbox", 100, 70, 4, 3),
+    ("cornellbox", 96, 80, 8, 4),
+    ("white-box", 80, 60, 8, 2),
+    ("CornellBox-Water-plastic", 48, 36, 8, 2),
+    ("CornellBox-Water-mirror", 40, 30, 3, 2),
+])
+def test_render_parity_precise(gpu, mrt_mod, oracle_mod, scene, W, H, L, frames):
+    sc, osc = _scene(mrt_mod, scene), _oscene(oracle_mod, mrt_mod, scene)
+    ref, A_ref = osc.render(W, H, L, SEED, frames, threads=8)
+    img, st = _render_gpu(mrt_mod, sc, W, H, L, frames, precise=True)
+    rel, rmse, same = pixel_metrics(img, ref)
+    print(f"{scene} {W}x{H} L={L} f={frames}: bit-identical {same:.5f}, rel<=1e-4 {np.mean(rel <= 1e-4):.5f}, "
+          f"rmse {rmse:.2e}, A gpu {st['active_ray_bounces']} oracle {A_ref}")
+    assert np.mean(rel <= 1e-4) >= 0.999
+    assert rmse <= 1e-3
+    assert abs(st["active_ray_bounces"] - A_ref) <= max(2, A_ref // 1000)
+    assert st["paths"] == W * H * frames
+
+
+@pytest.mark.parametrize("scene,L", [("cornellbox", 4), ("CornellBox-Water-plastic", 8)])
+def test_render_parity_fast(gpu, mrt_mod, oracle_mod, scene, L):
+    W, H, frames = 64, 48, 3
+    sc, osc = _scene(mrt_mod, scene), _oscene(oracle_mod, mrt_mod, scene)
+    ref, _ = osc.render(W, H, L, SEED, frames, threads=8)
+    img, _ = _render_gpu(mrt_mod, sc, W, H, L, frames, precise=False)
+    rel, rmse, same = pixel_metrics(img, ref)
+    print(f"fast {scene}: bit-identical {same:.4f}, rel<=1e-2 {np.mean(rel <= 1e-2):.5f}, rmse {rmse:.2e}")
+    assert np.mean(rel <= 1e-2) >= 0.99
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8])
+def test_shard_invariance(gpu, mrt_mod, shards):
+    """Tile-sharded renders summed == the 1-GPU image, bitwise."""
+    sc = _scene(mrt_mod, "cornellbox")
+    W, H, L, frames = 200, 150, 4, 2
+    full, st_full = _render_gpu(mrt_mod, sc, W, H, L, frames, precise=False)
+    acc = np.zeros_like(full)
+    paths = 0
+    for k in range(shards):
+        part, st = _render_gpu(mrt_mod, sc, W, H, L, frames, precise=False, shard=(k, shards))
+        acc[..., :3] += part[..., :3]
+        acc[..., 3] += part[..., 3]
+        paths += st["paths"]
+    assert paths == W * H * frames
+    assert np.array_equal(acc[..., :3], full[..., :3])
+    assert np.all(acc[..., 3] == 1.0)
+
+
+def test_deterministic_and_reset(gpu, mrt_mod):
+    sc = _scene(mrt_mod, "cornellbox")
+    r = mrt_mod.Renderer(sc, 320, 240, 4)
+    r.draw(3)
+    a = r.read_image()
+    r.reset()
+    r.draw(3)
+    b = r.read_image()
+    r.resize(160, 120)
+    r.draw(1)
+    c = r.read_image()
+    st = r.stats()
+    r.close()
+    assert a.tobytes() == b.tobytes()
+    assert c.shape == (120, 160, 4) and st["frame_index"] == 1 and np.isfinite(c).all()
+
+
+def test_save_image_roundtrip(gpu, mrt_mod, tmp_path):
+    import exr
+    sc = _scene(mrt_mod, "cornellbox")
+    r = mrt_mod.Renderer(sc, 64, 48, 2)
+    r.draw(2)
+    img = r.read_image()
+    r.save_current_image(str(tmp_path / "out.exr"))
+    r.save_current_image(str(tmp_path / "out.pfm"))
+    r.close()
+    back = exr.read_rgb(str(tmp_path / "out.exr"))[::-1]   # EXR is top-down
+    assert np.array_equal(back, img[..., :3])
+    with open(tmp_path / "out.pfm", "rb") as f:
+        header = f.readline() + f.readline() + f.readline()
+        data = np.frombuffer(f.read(), "<f4").reshape(48, 64, 3)
+    assert header.startswith(b"PF") and np.array_equal(data, img[..., :3])
