@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--precise", action="store_true", help="time the parity build instead of the fast build")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-frames", type=int, default=4, help="frames of the workload timed on the CPU oracle")
+    p.add_argument("--cpu-frames", type=int, default=8, help="frames of the workload timed on the CPU oracle")
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
     return p.parse_args()
 
@@ -84,23 +84,28 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     import torch
     import torch.distributed as dist
-    import mrt
 
     torch.cuda.set_device(local_rank)
+    torch.cuda.init()           # torch's HIP runtime first, then libmrt's (see mrt.py)
+    import mrt
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
     scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=local_rank)
+    # the accumulation image lives in a torch tensor so RCCL can reduce it in
+    # place; libmrt renders into it on its own stream (torch ships its own HIP
+    # runtime copy, so streams are not shared: r.sync() orders the reduce)
     image = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
-    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
     r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True, shard_rank=rank, shard_count=world,
-                     stream=stream.cuda_stream, image_ptr=image.data_ptr())
+                     image_ptr=image.data_ptr())
     r.prepare(spp)
 
     def step():
         r.reset()
         r.draw(spp)
         if world > 1:
+            r.sync()
             dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
 
     for _ in range(args.warmup):

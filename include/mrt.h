@@ -119,11 +119,13 @@ typedef struct mrt_renderer_desc {
   uint32_t shard_rank;             /* 64x64 tile t is rendered iff t % shard_count == shard_rank */
   uint32_t shard_count;            /* 0 or 1 = the whole frame */
   uint32_t flags;                  /* MRT_FLAG_* */
-  void* stream;                    /* optional external hipStream_t (NULL = own stream) */
+  void* stream;                    /* optional external hipStream_t of the SAME HIP runtime as
+                                      libmrt (NULL = own stream).  Never pass a stream created
+                                      by another runtime copy (e.g. PyTorch's bundled HIP). */
   float* image;                    /* optional external device image (W*H*4 floats), else owned */
 } mrt_renderer_desc;
 
-typedef struct mrt_stats {
+typedef struct mrt_stats {         /* counters are cumulative since create/resize */
   uint64_t frame_index;            /* frames accumulated since create/resize/reset */
   uint64_t paths;                  /* pixel paths traced by this renderer (owned pixels x frames) */
   uint64_t active_ray_bounces;     /* A: rays alive at the start of each bounce, summed */
@@ -137,7 +139,8 @@ typedef struct mrt_stats {
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);
 /* drawableSizeWillChange: reallocate, frameIndex = 0 (Renderer.mm:640-657) */
 int mrt_renderer_resize(mrt_renderer* r, uint32_t width, uint32_t height);
-/* frameIndex = 0 without reallocating (the next frame overwrites the image) */
+/* frameIndex = 0 without reallocating (the next frame overwrites the image);
+ * the cumulative counters of mrt_stats are kept. */
 int mrt_renderer_reset(mrt_renderer* r);
 /* Generate + upload the noise tables for frames [frame_index, frame_index+n)
  * ahead of time (the reference regenerates one slot per frame on the CPU,
@@ -163,6 +166,9 @@ int mrt_abi_version(void);
 /* The deterministic noise table of SURVEY.md A.3 for frame `frame` (-1 = the
  * initial table), 64*64*4 floats, host memory. */
 int mrt_noise_table(uint64_t seed, int64_t frame, float* out16384);
+/* Wait for work queued by libmrt on `stream` (NULL = everything on the device
+ * libmrt's runtime has queued). */
+int mrt_synchronize(void* stream);
 /* Number of HIP devices visible (0 when none; never fails). */
 int mrt_device_count(void);
 

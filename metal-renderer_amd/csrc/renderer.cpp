@@ -280,6 +280,12 @@ int mrt_device_count(void) {
   return n;
 }
 
+int mrt_synchronize(void* stream) {
+  if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  else HIP_TRY(hipDeviceSynchronize());
+  return MRT_OK;
+}
+
 int mrt_noise_table(uint64_t seed, int64_t frame, float* out) {
   if (!out) return fail(MRT_ERR_INVALID, "null output");
   mrt::make_noise_table(seed, frame, out);
@@ -563,9 +569,7 @@ int mrt_renderer_reset(mrt_renderer* r) {
   if (rc) return rc;
   HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)r->desc.width * r->desc.height * 16, r->stream));
   r->frame_index = 0;
-  const uint64_t owned = r->owned_pixels;
-  r->stats = mrt_stats{};
-  r->stats.owned_pixels = owned;
+  r->stats.frame_index = 0;   // cumulative counters (paths, A, kernel time) persist
   return MRT_OK;
 }
 

@@ -15,6 +15,12 @@ which take device pointers (ints) to reference-layout AoS buffers.
 This module only binds the native library: every call runs the HIP kernels in
 libmrt.so.  There is no CPU fallback; if the library is missing the import
 fails loudly.
+
+Interop note: PyTorch-ROCm wheels bundle their own copy of the HIP runtime.
+Both copies share the process's HSA runtime, so device pointers (torch tensors)
+can be handed to libmrt, but (1) torch must initialise its runtime before
+libmrt is first used in a process that uses both, and (2) torch stream handles
+must not be passed to libmrt (synchronise with Renderer.sync() instead).
 """
 from __future__ import annotations
 
@@ -89,7 +95,7 @@ EXPORTED = [
     "mrt_renderer_create", "mrt_renderer_resize", "mrt_renderer_reset", "mrt_renderer_prepare",
     "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image",
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
-    "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count",
+    "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
 ]
 
 _lib = None
@@ -135,6 +141,7 @@ def lib() -> ctypes.CDLL:
         "mrt_abi_version": [],
         "mrt_noise_table": [u64, i64, vp],
         "mrt_device_count": [],
+        "mrt_synchronize": [vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -279,30 +286,52 @@ class Renderer:
 
 
 # ---- stage-level ABI (device pointers, reference AoS layouts) -------------
-def raygen(scene: Scene, width: int, height: int, noise_ptr: int, rays_ptr: int, precise=True, stream=None):
-    _check(lib().mrt_raygen(scene.handle, width, height, noise_ptr, rays_ptr, FLAG_PRECISE if precise else 0, stream),
-           "mrt_raygen")
+# Each call launches on `stream` (None = libmrt's default stream) and, unless
+# sync=False, waits for it with mrt_synchronize (torch.cuda.synchronize() does
+# not see libmrt's runtime copy).
+def synchronize(stream=None) -> None:
+    _check(lib().mrt_synchronize(stream), "mrt_synchronize")
 
 
-def intersect(scene: Scene, rays_ptr: int, stride: int, count: int, isect_ptr: int, precise=True, stream=None):
-    _check(lib().mrt_intersect(scene.handle, rays_ptr, stride, count, isect_ptr, FLAG_PRECISE if precise else 0,
-                               stream), "mrt_intersect")
+def _flags(precise):
+    return FLAG_PRECISE if precise else 0
+
+
+def raygen(scene: Scene, width: int, height: int, noise_ptr: int, rays_ptr: int, precise=True, stream=None,
+           sync=True):
+    _check(lib().mrt_raygen(scene.handle, width, height, noise_ptr, rays_ptr, _flags(precise), stream), "mrt_raygen")
+    if sync:
+        synchronize(stream)
+
+
+def intersect(scene: Scene, rays_ptr: int, stride: int, count: int, isect_ptr: int, precise=True, stream=None,
+              sync=True):
+    _check(lib().mrt_intersect(scene.handle, rays_ptr, stride, count, isect_ptr, _flags(precise), stream),
+           "mrt_intersect")
+    if sync:
+        synchronize(stream)
 
 
 def shade(scene: Scene, width, height, frame_index, max_path_length, noise_ptr, isect_ptr, rays_ptr, srays_ptr,
-          precise=True, stream=None):
+          precise=True, stream=None, sync=True):
     _check(lib().mrt_shade(scene.handle, width, height, frame_index, max_path_length, noise_ptr, isect_ptr, rays_ptr,
-                           srays_ptr, FLAG_PRECISE if precise else 0, stream), "mrt_shade")
+                           srays_ptr, _flags(precise), stream), "mrt_shade")
+    if sync:
+        synchronize(stream)
 
 
-def resolve_shadow(scene: Scene, count, isect_ptr, rays_ptr, srays_ptr, precise=True, stream=None):
-    _check(lib().mrt_resolve_shadow(scene.handle, count, isect_ptr, rays_ptr, srays_ptr,
-                                    FLAG_PRECISE if precise else 0, stream), "mrt_resolve_shadow")
+def resolve_shadow(scene: Scene, count, isect_ptr, rays_ptr, srays_ptr, precise=True, stream=None, sync=True):
+    _check(lib().mrt_resolve_shadow(scene.handle, count, isect_ptr, rays_ptr, srays_ptr, _flags(precise), stream),
+           "mrt_resolve_shadow")
+    if sync:
+        synchronize(stream)
 
 
-def accumulate(scene: Scene, width, height, frame_index, rays_ptr, image_ptr, precise=True, stream=None):
-    _check(lib().mrt_accumulate(scene.handle, width, height, frame_index, rays_ptr, image_ptr,
-                                FLAG_PRECISE if precise else 0, stream), "mrt_accumulate")
+def accumulate(scene: Scene, width, height, frame_index, rays_ptr, image_ptr, precise=True, stream=None, sync=True):
+    _check(lib().mrt_accumulate(scene.handle, width, height, frame_index, rays_ptr, image_ptr, _flags(precise),
+                                stream), "mrt_accumulate")
+    if sync:
+        synchronize(stream)
 
 
 def noise_table(seed: int, frame: int):

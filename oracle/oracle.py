@@ -138,6 +138,8 @@ class OracleScene:
     # ---- stages (renderer/Shaders.metal) ----
     def intersect(self, rays: np.ndarray) -> np.ndarray:
         rays = np.ascontiguousarray(rays)
+        if rays.dtype.itemsize not in (RAY_DTYPE.itemsize, SRAY_DTYPE.itemsize):
+            raise ValueError(f"ray records must be Ray (80 B) or LightSamplingRay (48 B), got {rays.dtype.itemsize} B")
         out = np.zeros(len(rays), ISECT_DTYPE)
         lib().orc_intersect(self.h, _p(rays), rays.dtype.itemsize, len(rays), _p(out))
         return out

@@ -35,5 +35,7 @@ def gpu(mrt_mod):
     """Skip-free GPU gate: a -m gpu run on a box without a device must FAIL."""
     import torch
     assert torch.cuda.is_available(), "gpu test run without a visible HIP device"
+    torch.cuda.init()   # torch's bundled HIP runtime must initialise before libmrt's
+    torch.zeros(1, device="cuda")
     assert mrt_mod.device_count() > 0, "libmrt.so sees no HIP device"
     return torch
