@@ -169,6 +169,10 @@ int mrt_noise_table(uint64_t seed, int64_t frame, float* out16384);
 /* Wait for work queued by libmrt on `stream` (NULL = everything on the device
  * libmrt's runtime has queued). */
 int mrt_synchronize(void* stream);
+/* Diagnostics: cycles spent per phase of the bounce loop, summed over waves
+ * (out[0..4] = load, trace, shade, shadow, finish; out[5] = wave iterations).
+ * Non-zero only in the separately built stamp library (make stamps). */
+int mrt_debug_stamps(uint64_t* out8, int reset);
 /* Number of HIP devices visible (0 when none; never fails). */
 int mrt_device_count(void);
 

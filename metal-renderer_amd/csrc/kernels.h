@@ -29,9 +29,17 @@ struct BounceArgs {
   uint32_t bounce;             // loop iteration i (renderer/Renderer.mm:517)
   uint32_t max_path_length;    // MAX_PATH_LENGTH
   uint32_t shard_rank, shard_count, tiles_x;
-  uint32_t num_slots;          // bounce 0: owned tiles * 4096 pixel slots
-  const uint32_t* in_count;    // bounce > 0: live rays produced by the previous bounce
-  uint32_t* out_count;         // live rays produced by this bounce (atomic)
+  uint32_t num_slots;          // bounce 0 input: owned tiles * 4096 pixel slots
+  uint32_t debug;              // ablation bits for profiling (0 in production, env MRT_DEBUG):
+                               //   1 = skip shadow traversal, 2 = skip shading, 4 = no queue writes
+  // segmented queues: block g of a launch appends its survivors to slots
+  // [g*chunk, g*chunk + count_g) of the output queue
+  uint32_t in_segments;        // bounce > 0: number of input segments (previous grid size)
+  const uint32_t* in_seg_count;
+  const uint32_t* in_chunk;    // previous launch's chunk (segment stride in slots)
+  uint32_t* out_seg_count;     // [grid]
+  uint32_t* out_chunk;
+  uint32_t* out_total;         // survivors of this launch (stats)
   RayQueue in_q, out_q;
   const float4* noise_raygen;  // slot f%3  = T_f
   const float4* noise_shade;   // slot (f+i)%3
@@ -50,9 +58,13 @@ struct BounceArgs {
                             const RefShadowRay* srays, hipStream_t s);                                    \
   hipError_t launch_accumulate(uint32_t W, uint32_t H, uint32_t frame_index, const RefRay* rays,          \
                                float* image, hipStream_t s);                                              \
-  /* fused wavefront bounce; grid = 0 -> persistent grid from occupancy */                               \
+  /* persistent grid size of the fused bounce kernel for this scene */                                    \
+  hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                 \
+  /* fused wavefront bounce over `grid` blocks (the same grid for every launch of a renderer) */          \
   hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
-                           hipStream_t s);                                                                \
+                           uint32_t grid, hipStream_t s);                                                 \
+  /* diagnostic phase stamps (MRT_STAMPS builds; zeros otherwise) */                                      \
+  hipError_t read_stamps(unsigned long long* out8, bool reset);                                          \
   }
 
 MRT_DECLARE_LAUNCHERS(precise)

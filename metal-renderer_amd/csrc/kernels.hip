@@ -26,6 +26,9 @@ namespace MRT_NS {
 namespace {
 
 constexpr int kBlock = 256;   // 4 waves of 64 lanes
+#ifndef MRT_BOUNCE_WAVES
+#define MRT_BOUNCE_WAVES 1
+#endif
 
 // ---------------------------------------------------------------------------
 // scalar math (precision policy)
@@ -160,40 +163,142 @@ __device__ __forceinline__ void box2(const float4& a, const float4& b, const flo
   hr = tnr <= tfr;
 }
 
-// Traversal context: LDS-staged top nodes + a per-lane LDS stack laid out
-// [entry][lane] (consecutive lanes hit consecutive banks).
-struct TraversalCtx {
-  const float4* lds_nodes;
-  uint32_t n_lds;
-  uint32_t* stack;       // &lds_stack[threadIdx.x]
+// LDS staging modes:
+//   kGlobal  — only the per-lane traversal stack lives in LDS (stage ABI kernels);
+//   kTopLds  — the first n BFS-ordered BVH nodes (top levels) are staged in
+//              LDS; deeper nodes, leaf triangles and shading records are read
+//              from global memory (L2 / Infinity Cache / HBM);
+//   kAllLds  — small scenes: every node, leaf triangle, per-primitive shading
+//              record, material and light entry is staged in LDS once per
+//              block, so traversal and shading never leave the CU.
+// LDS image: [nodes][triangles][prims][materials][lights] as float4, then the
+// uint32 scratch (segment prefix), then the stack laid out [entry][lane]
+// (consecutive lanes hit consecutive banks).  All LDS accesses index the
+// __shared__ symbol directly so they lower to ds_read/ds_write (a pointer
+// select between LDS and global lowers to flat_load).
+enum LdsMode { kGlobal = 0, kTopLds = 1, kAllLds = 2 };
+extern __shared__ float4 g_lds[];
+
+struct LdsCtx {
+  uint32_t n_lds_nodes;   // nodes [0, n) are in LDS
+  uint32_t tri_base;      // float4 offsets (kAllLds)
+  uint32_t prim_base;
+  uint32_t mat_base;
+  uint32_t light_base;
+  uint32_t scratch_base;  // uint32 offset of the per-block scratch
+  uint32_t stack_base;    // uint32 offset of this lane's stack slot 0
 };
 
-__device__ __forceinline__ void fetch_node(const DeviceScene& sc, const TraversalCtx& cx, int32_t node, float4& a,
+__device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
+
+// float4 counts of the staged scene image for a mode
+__host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t nodes, uint32_t lds_nodes, uint32_t tris,
+                                                      uint32_t mats, uint32_t lights) {
+  if (mode == kAllLds) return 4 * nodes + 3 * tris + 6 * tris + 2 * mats + 7 * lights;
+  if (mode == kTopLds) return 4 * lds_nodes;
+  return 0;
+}
+
+template <int MODE>
+__device__ __forceinline__ void fetch_node(const DeviceScene& sc, const LdsCtx& cx, int32_t node, float4& a,
                                            float4& b, float4& c, float4& e) {
-  const float4* p = ((uint32_t)node < cx.n_lds) ? cx.lds_nodes + 4 * node
-                                                : reinterpret_cast<const float4*>(sc.nodes) + 4 * (size_t)node;
-  a = p[0];
-  b = p[1];
-  c = p[2];
-  e = p[3];
+  if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
+    a = g_lds[4 * node];
+    b = g_lds[4 * node + 1];
+    c = g_lds[4 * node + 2];
+    e = g_lds[4 * node + 3];
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 4 * (size_t)node;
+    a = p[0];
+    b = p[1];
+    c = p[2];
+    e = p[3];
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void fetch_tri(const DeviceScene& sc, const LdsCtx& cx, uint32_t k, float4& t0,
+                                          float4& t1, float4& t2) {
+  if (MODE == kAllLds) {
+    t0 = g_lds[cx.tri_base + 3 * k];
+    t1 = g_lds[cx.tri_base + 3 * k + 1];
+    t2 = g_lds[cx.tri_base + 3 * k + 2];
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(sc.tris) + 3 * (size_t)k;
+    t0 = p[0];
+    t1 = p[1];
+    t2 = p[2];
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ float4 fetch_prim(const DeviceScene& sc, const LdsCtx& cx, uint32_t prim, uint32_t i) {
+  if (MODE == kAllLds) return g_lds[cx.prim_base + 6 * prim + i];
+  return reinterpret_cast<const float4*>(sc.prims)[6 * (size_t)prim + i];
+}
+template <int MODE>
+__device__ __forceinline__ float4 fetch_mat(const DeviceScene& sc, const LdsCtx& cx, uint32_t m, uint32_t i) {
+  if (MODE == kAllLds) return g_lds[cx.mat_base + 2 * m + i];
+  return reinterpret_cast<const float4*>(sc.materials)[2 * m + i];
+}
+template <int MODE>
+__device__ __forceinline__ float4 fetch_light(const DeviceScene& sc, const LdsCtx& cx, uint32_t l, uint32_t i) {
+  if (MODE == kAllLds) return g_lds[cx.light_base + 7 * l + i];
+  return reinterpret_cast<const float4*>(sc.lights)[7 * l + i];
+}
+
+__device__ __forceinline__ void stack_push(const LdsCtx& cx, int sp, int32_t v) {
+  lds_u32()[cx.stack_base + sp * kBlock] = (uint32_t)v;
+}
+__device__ __forceinline__ int32_t stack_get(const LdsCtx& cx, int sp) {
+  return (int32_t)lds_u32()[cx.stack_base + sp * kBlock];
+}
+
+// Stage the LDS image for `MODE` (every thread of the block calls it);
+// `scratch_u32` uint32 words of per-block scratch follow the scene image.
+template <int MODE>
+__device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scratch_u32) {
+  LdsCtx cx;
+  const uint32_t n_nodes = (MODE == kAllLds) ? sc.num_nodes : (MODE == kTopLds ? sc.lds_nodes : 0u);
+  const uint32_t T = (MODE == kAllLds) ? sc.num_triangles : 0u;
+  const uint32_t M = (MODE == kAllLds) ? sc.num_materials : 0u;
+  const uint32_t NL = (MODE == kAllLds) ? sc.num_lights + 1 : 0u;
+  cx.n_lds_nodes = n_nodes;
+  cx.tri_base = 4 * n_nodes;
+  cx.prim_base = cx.tri_base + 3 * T;
+  cx.mat_base = cx.prim_base + 6 * T;
+  cx.light_base = cx.mat_base + 2 * M;
+  const uint32_t f4 = cx.light_base + 7 * NL;
+  cx.scratch_base = 4 * f4;
+  cx.stack_base = cx.scratch_base + ((scratch_u32 + 3) & ~3u) + threadIdx.x;
+  if (MODE != kGlobal) {
+    const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes), reinterpret_cast<const float4*>(sc.tris),
+                            reinterpret_cast<const float4*>(sc.prims), reinterpret_cast<const float4*>(sc.materials),
+                            reinterpret_cast<const float4*>(sc.lights)};
+    const uint32_t base[5] = {0u, cx.tri_base, cx.prim_base, cx.mat_base, cx.light_base};
+    const uint32_t len[5] = {4 * n_nodes, 3 * T, 6 * T, 2 * M, 7 * NL};
+    for (int r = 0; r < 5; ++r)
+      for (uint32_t i = threadIdx.x; i < len[r]; i += kBlock) g_lds[base[r] + i] = src[r][i];
+    __syncthreads();
+  }
+  return cx;
 }
 
 // Nearest hit in [tmin, tmax]; ties -> lowest primitive index.
-template <int STACK>
-__device__ Hit trace_nearest(const DeviceScene& sc, const TraversalCtx& cx, V3 o, V3 d, float tmin, float tmax) {
+template <int STACK, int MODE>
+__device__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, float tmax) {
   Hit h;
   h.t = tmax;
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
   const RayBox rb = make_raybox(o, d);
-  const float4* tris = reinterpret_cast<const float4*>(sc.tris);
   int32_t node = sc.root;
   int sp = 0;
   while (true) {
     if (node >= 0) {
       float4 a, b, c, e;
-      fetch_node(sc, cx, node, a, b, c, e);
+      fetch_node<MODE>(sc, cx, node, a, b, c, e);
       bool hl, hr;
       float tnl, tnr;
       box2(a, b, c, o, rb, tmin, h.t, hl, hr, tnl, tnr);
@@ -201,7 +306,7 @@ __device__ Hit trace_nearest(const DeviceScene& sc, const TraversalCtx& cx, V3 o
       if (hl && hr) {
         const bool swap = tnr < tnl;
         const int32_t nearer = swap ? rr : rl, farther = swap ? rl : rr;
-        if (sp < STACK) { cx.stack[sp * kBlock] = (uint32_t)farther; ++sp; }
+        if (sp < STACK) { stack_push(cx, sp, farther); ++sp; }
         node = nearer;
         continue;
       }
@@ -211,7 +316,8 @@ __device__ Hit trace_nearest(const DeviceScene& sc, const TraversalCtx& cx, V3 o
       const uint32_t leaf = ~(uint32_t)node;
       const uint32_t first = leaf >> kLeafCountBits, cnt = (leaf & (kMaxLeafSize - 1)) + 1;
       for (uint32_t k = 0; k < cnt; ++k) {
-        const float4 t0 = tris[3 * (first + k)], t1 = tris[3 * (first + k) + 1], t2 = tris[3 * (first + k) + 2];
+        float4 t0, t1, t2;
+        fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
         float t, u, v;
         if (tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v)) {
           const uint32_t prim = fbits(t0.w);
@@ -227,24 +333,23 @@ __device__ Hit trace_nearest(const DeviceScene& sc, const TraversalCtx& cx, V3 o
     }
     if (sp == 0) break;
     --sp;
-    node = (int32_t)cx.stack[sp * kBlock];
+    node = stack_get(cx, sp);
   }
   return h;
 }
 
 // Is any primitive k != target hit with (t_k, k) < (t_target, target)?
 // (the shadow ray's MPS nearest hit is then not the target)
-template <int STACK>
-__device__ bool trace_occluded(const DeviceScene& sc, const TraversalCtx& cx, V3 o, V3 d, uint32_t target,
+template <int STACK, int MODE>
+__device__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
                                float t_target) {
   const RayBox rb = make_raybox(o, d);
-  const float4* tris = reinterpret_cast<const float4*>(sc.tris);
   int32_t node = sc.root;
   int sp = 0;
   while (true) {
     if (node >= 0) {
       float4 a, b, c, e;
-      fetch_node(sc, cx, node, a, b, c, e);
+      fetch_node<MODE>(sc, cx, node, a, b, c, e);
       bool hl, hr;
       float tnl, tnr;
       box2(a, b, c, o, rb, 0.0f, t_target, hl, hr, tnl, tnr);
@@ -252,7 +357,7 @@ __device__ bool trace_occluded(const DeviceScene& sc, const TraversalCtx& cx, V3
       if (hl && hr) {
         const bool swap = tnr < tnl;
         const int32_t nearer = swap ? rr : rl, farther = swap ? rl : rr;
-        if (sp < STACK) { cx.stack[sp * kBlock] = (uint32_t)farther; ++sp; }
+        if (sp < STACK) { stack_push(cx, sp, farther); ++sp; }
         node = nearer;
         continue;
       }
@@ -262,7 +367,8 @@ __device__ bool trace_occluded(const DeviceScene& sc, const TraversalCtx& cx, V3
       const uint32_t leaf = ~(uint32_t)node;
       const uint32_t first = leaf >> kLeafCountBits, cnt = (leaf & (kMaxLeafSize - 1)) + 1;
       for (uint32_t k = 0; k < cnt; ++k) {
-        const float4 t0 = tris[3 * (first + k)], t1 = tris[3 * (first + k) + 1], t2 = tris[3 * (first + k) + 2];
+        float4 t0, t1, t2;
+        fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
         const uint32_t prim = fbits(t0.w);
         if (prim == target) continue;
         float t, u, v;
@@ -272,7 +378,7 @@ __device__ bool trace_occluded(const DeviceScene& sc, const TraversalCtx& cx, V3
     }
     if (sp == 0) break;
     --sp;
-    node = (int32_t)cx.stack[sp * kBlock];
+    node = stack_get(cx, sp);
   }
   return false;
 }
@@ -280,14 +386,14 @@ __device__ bool trace_occluded(const DeviceScene& sc, const TraversalCtx& cx, V3
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
 // (renderer/Shaders.metal:214-231): contributes iff the nearest hit of the
 // shadow ray (tmin 0, tmax inf) is the target triangle at t >= 1e-4.
-template <int STACK>
-__device__ bool shadow_reaches_target(const DeviceScene& sc, const TraversalCtx& cx, V3 o, V3 d, uint32_t target) {
-  const float4* pr = reinterpret_cast<const float4*>(sc.prims) + 6 * (size_t)target;
-  const V3 p0 = mk(pr[0]), p1 = mk(pr[1]), p2 = mk(pr[2]);
+template <int STACK, int MODE>
+__device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target) {
+  const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
+  const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
   float tT, u, v;
   if (!tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v)) return false;
   if (!(tT >= kDistanceEpsilon)) return false;
-  return !trace_occluded<STACK>(sc, cx, o, d, target, tT);
+  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT);
 }
 
 // ---------------------------------------------------------------------------
@@ -349,9 +455,9 @@ struct Mat {
   float ior;
   uint32_t type;
 };
-__device__ __forceinline__ Mat load_material(const DeviceScene& sc, uint32_t m) {
-  const float4* p = reinterpret_cast<const float4*>(sc.materials) + 2 * m;
-  const float4 a = p[0], b = p[1];
+template <int MODE>
+__device__ __forceinline__ Mat load_material(const DeviceScene& sc, const LdsCtx& cx, uint32_t m) {
+  const float4 a = fetch_mat<MODE>(sc, cx, m, 0), b = fetch_mat<MODE>(sc, cx, m, 1);
   return {mk(a), mk(b), a.w, fbits(b.w)};
 }
 
@@ -421,11 +527,13 @@ __device__ __forceinline__ float lightTriangleSamplePDF(float tpdf, float area, 
 // selectLightTriangle — KernelHelpers.h:49-54.  The linear scan returns the
 // first index with !(cdf[index+1] <= xi) (or count); cdf is non-decreasing, so
 // a binary search returns the same index.
-__device__ __forceinline__ uint32_t selectLightTriangle(const float4* lights, uint32_t count, float xi) {
+template <int MODE>
+__device__ __forceinline__ uint32_t selectLightTriangle(const DeviceScene& sc, const LdsCtx& cx, uint32_t count,
+                                                        float xi) {
   uint32_t lo = 0, hi = count;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (lights[7 * (mid + 1) + 2].w <= xi) lo = mid + 1;   // entry mid+1: (v1.n, cdf)
+    if (fetch_light<MODE>(sc, cx, mid + 1, 2).w <= xi) lo = mid + 1;   // entry mid+1: (v1.n, cdf)
     else hi = mid;
   }
   return lo;
@@ -468,25 +576,28 @@ __device__ __forceinline__ uint32_t shade_noise_cell(uint32_t x, uint32_t y, uin
 // renderer/Shaders.metal:128-211.  Emits the NEE shadow ray (when
 // bounce + 1 < L), adds MIS-weighted emission, and — when `next` — samples
 // the next bounce and updates the throughput.
-__device__ __forceinline__ void shade_hit(const DeviceScene& sc, const Hit& h, PathState& s, const float4& ns,
-                                          uint32_t bounce, uint32_t L, bool next, ShadowRay& sh) {
-  const float4* pr = reinterpret_cast<const float4*>(sc.prims) + 6 * (size_t)h.prim;
-  const float4 P0 = pr[0], P1 = pr[1], P2 = pr[2], N0 = pr[3], N1 = pr[4], N2 = pr[5];
+template <int MODE>
+__device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& cx, const Hit& h, PathState& s,
+                                          const float4& ns, uint32_t bounce, uint32_t L, bool next, ShadowRay& sh) {
+  const float4 P0 = fetch_prim<MODE>(sc, cx, h.prim, 0), P1 = fetch_prim<MODE>(sc, cx, h.prim, 1);
+  const float4 P2 = fetch_prim<MODE>(sc, cx, h.prim, 2), N0 = fetch_prim<MODE>(sc, cx, h.prim, 3);
+  const float4 N1 = fetch_prim<MODE>(sc, cx, h.prim, 4), N2 = fetch_prim<MODE>(sc, cx, h.prim, 5);
   const uint32_t mat_index = fbits(P0.w);
   const uint32_t light_index = fbits(P1.w);
-  const Mat m = load_material(sc, mat_index);
+  const Mat m = load_material<MODE>(sc, cx, mat_index);
   // interpolate(float2) — KernelHelpers.h:23-47
   const float wu = h.u, wv = h.v, ww = (1.0f - h.u) - h.v;
   const V3 hv = add(add(mul(mk(P0), wu), mul(mk(P1), wv)), mul(mk(P2), ww));
   const V3 hn = normalize(add(add(mul(mk(N0), wu), mul(mk(N1), wv)), mul(mk(N2), ww)));
   const V3 wI = s.d;
-  const float4* lights = reinterpret_cast<const float4*>(sc.lights);
   sh.valid = false;
   // light sampling — Shaders.metal:150-176
   if (bounce + 1 < L) {
-    const uint32_t li = selectLightTriangle(lights, sc.num_lights, ns.z);
-    const float4* lt = lights + 7 * li;
-    const float4 LA = lt[0], LB = lt[1], LC = lt[2], LD = lt[3], LE = lt[4], LF = lt[5], LG = lt[6];
+    const uint32_t li = selectLightTriangle<MODE>(sc, cx, sc.num_lights, ns.z);
+    const float4 LA = fetch_light<MODE>(sc, cx, li, 0), LB = fetch_light<MODE>(sc, cx, li, 1);
+    const float4 LC = fetch_light<MODE>(sc, cx, li, 2), LD = fetch_light<MODE>(sc, cx, li, 3);
+    const float4 LE = fetch_light<MODE>(sc, cx, li, 4), LF = fetch_light<MODE>(sc, cx, li, 5);
+    const float4 LG = fetch_light<MODE>(sc, cx, li, 6);
     // barycentric(noise.wx) — Raytracing.h:182-187
     const float r1 = m_sqrt(ns.w), r2 = ns.x;
     const float bu = 1.0f - r1, bv = r1 * (1.0f - r2), bw = r1 * r2;
@@ -509,8 +620,7 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const Hit& h, P
   // emission with MIS — Shaders.metal:180-197 (the light vertex re-derived
   // there is the hit vertex itself: lights[ref.lightTriangleIndex].index == prim)
   if (light_index != 0xFFFFFFFFu) {
-    const float4* lt = lights + 7 * light_index;
-    const float area = lt[0].w, tpdf = lt[1].w;
+    const float area = fetch_light<MODE>(sc, cx, light_index, 0).w, tpdf = fetch_light<MODE>(sc, cx, light_index, 1).w;
     V3 dirToLight;
     const float mPdf = s.pdf;
     const float lPdf = s.prevDiffuse * lightTriangleSamplePDF(tpdf, area, s.o, hv, hn, dirToLight);
@@ -546,44 +656,131 @@ __device__ __forceinline__ void accumulate_pixel(float4* image, uint32_t pix, V3
 }
 
 // ---------------------------------------------------------------------------
+// Diagnostic phase stamps (MRT_STAMPS builds only; never in the product):
+// s_memtime around each wave-uniform phase of the bounce loop, summed per
+// wave in SGPRs and added once per wave into g_stamps at kernel exit.  The
+// stamp waits for vmcnt/lgkmcnt(0), so read the SHARES, not the length.
+// ---------------------------------------------------------------------------
+#ifndef MRT_STAMPS
+#define MRT_STAMPS 0
+#endif
+#if MRT_STAMPS
+__device__ unsigned long long g_stamps[8];
+__device__ __forceinline__ uint64_t stamp_now() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP_DECL() uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}; uint64_t st_prev = 0; uint64_t st_iters = 0
+#define STAMP_BEGIN() do { st_prev = stamp_now(); ++st_iters; } while (0)
+#define STAMP(k) do { const uint64_t t_ = stamp_now(); st_acc[k] += t_ - st_prev; st_prev = t_; } while (0)
+#define STAMP_FLUSH() do { if ((threadIdx.x & 63u) == 0) { \
+    for (int k_ = 0; k_ < 5; ++k_) atomicAdd(&g_stamps[k_], (unsigned long long)st_acc[k_]); \
+    atomicAdd(&g_stamps[5], (unsigned long long)st_iters); } } while (0)
+#else
+#define STAMP_DECL() do {} while (0)
+#define STAMP_BEGIN() do {} while (0)
+#define STAMP(k) do {} while (0)
+#define STAMP_FLUSH() do {} while (0)
+#endif
+
+// ---------------------------------------------------------------------------
 // Fused wavefront bounce kernel (the hot path).
 //
-// One launch per (frame, bounce).  Each ray slot: [bounce 0: generate camera
-// ray | else load SoA state] -> nearest hit -> shade (NEE shadow ray, MIS
-// emission, next direction) -> shadow visibility -> either accumulate the
-// pixel (path ends: miss, near hit, or last bounce) or append the ray to the
-// next queue.  Appends are compacted per wave with a ballot + popcount
-// prefix and ONE atomicAdd per wave.  Lanes are processed in wave-uniform
-// grid-stride chunks so every ballot sees a converged wave.
+// One launch per (frame, bounce) over a persistent grid of G blocks.  Each
+// ray: [bounce 0: generate the camera ray | else load its SoA state] ->
+// nearest hit -> shade (NEE shadow ray, MIS emission, next direction) ->
+// shadow visibility -> either accumulate the pixel (path ends: miss, near
+// hit, or last bounce) or append the ray to the next queue.
+//
+// Queue compaction without global atomics: the N input rays are split into
+// G contiguous block ranges of `chunk` rays; block g appends its survivors to
+// [g*chunk, g*chunk + count_g) of the next queue with one LDS atomic per wave
+// (ballot + popcount prefix inside the wave), and publishes count_g once.
+// The next launch prefix-scans the G counts in LDS and maps its own dense
+// index i to (segment j, offset) with a binary search.  Ray order inside a
+// block segment is not deterministic; every ray carries its pixel, so the
+// image is.
 // ---------------------------------------------------------------------------
-template <int STACK>
-__global__ __launch_bounds__(kBlock) void bounce_kernel(DeviceScene sc, BounceArgs a) {
-  extern __shared__ float4 lds[];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t n_lds = sc.lds_nodes;
-  for (uint32_t i = tid; i < 4 * n_lds; i += kBlock) lds[i] = reinterpret_cast<const float4*>(sc.nodes)[i];
+// exclusive prefix of v[0..n) in place (LDS), returns the total; n <= 16*kBlock
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wave_tmp) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t per = (n + kBlock - 1) / kBlock;
+  const uint32_t b = tid * per, e = min(n, b + per);
+  uint32_t local = 0;
+  for (uint32_t i = b; i < e; ++i) local += v[i];
+  uint32_t incl = local;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t up = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += up;
+  }
+  if (lane == 63) wave_tmp[wave] = incl;
   __syncthreads();
-  TraversalCtx cx;
-  cx.lds_nodes = lds;
-  cx.n_lds = n_lds;
-  cx.stack = reinterpret_cast<uint32_t*>(lds + 4 * n_lds) + tid;
+  uint32_t wave_prefix = 0, total = 0;
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    if (w < wave) wave_prefix += wave_tmp[w];
+    total += wave_tmp[w];
+  }
+  uint32_t run = wave_prefix + incl - local;
+  for (uint32_t i = b; i < e; ++i) {
+    const uint32_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+  __syncthreads();
+  return total;
+}
+
+template <int STACK, int MODE>
+__global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
+  __shared__ uint32_t s_wave[kBlock / 64];
+  __shared__ uint32_t s_cursor;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t G = gridDim.x;
+  const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
+  const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1);
+  uint32_t* seg = lds_u32() + cx.scratch_base;   // exclusive prefix of the input segments
+  if (tid == 0) s_cursor = 0;
+
+  uint32_t N, in_chunk = 0;
+  if (a.bounce == 0) {
+    N = a.num_slots;
+    __syncthreads();
+  } else {
+    for (uint32_t i = tid; i < nseg; i += kBlock) seg[i] = a.in_seg_count[i];
+    __syncthreads();
+    N = block_exclusive_scan(seg, nseg, s_wave);
+    in_chunk = *a.in_chunk;
+  }
+  const uint32_t chunk = ((N + G - 1) / G + kBlock - 1) / kBlock * kBlock;
+  const uint32_t begin = min(N, blockIdx.x * chunk), end = min(N, begin + chunk);
+  const uint32_t out_base = blockIdx.x * chunk;
+  // segments overlapping this block's range (narrow: segments are ~chunk long)
+  uint32_t seg_lo = 0, seg_hi = nseg;
+  if (nseg) {
+    uint32_t lo = 0, hi = nseg;   // last j with seg[j] <= begin
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= begin) lo = mid; else hi = mid; }
+    seg_lo = lo;
+  }
 
   const uint32_t lane = tid & 63u;
-  const uint32_t wave_in_grid = blockIdx.x * (kBlock / 64) + (tid >> 6);
-  const uint32_t wave_stride = gridDim.x * kBlock;
-  const uint32_t count = (a.bounce == 0) ? a.num_slots : *a.in_count;
   const bool last = (a.bounce + 1 == a.max_path_length);
   const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
-  for (uint32_t base = wave_in_grid * 64; base < count; base += wave_stride) {
-    const uint32_t slot = base + lane;
-    bool active = slot < count;
+  STAMP_DECL();
+  for (uint32_t base = begin + (tid & ~63u); base < end; base += kBlock) {
+    STAMP_BEGIN();
+    // -- phase 0: generate (bounce 0) or load (SoA queue) the ray state
+    const uint32_t idx = base + lane;
+    bool active = idx < end;
     PathState s;
     uint32_t pix = 0, x = 0, y = 0;
     if (active) {
       if (a.bounce == 0) {
         // owned tile k -> global tile rank + k*count; 8x8 pixel blocks per wave
-        const uint32_t k = slot >> 12, p = slot & 4095u;
+        const uint32_t k = idx >> 12, p = idx & 4095u;
         const uint32_t t = a.shard_rank + k * a.shard_count;
         const uint32_t tx = t % a.tiles_x, ty = t / a.tiles_x;
         const uint32_t blk = p >> 6, q = p & 63u;
@@ -601,6 +798,9 @@ __global__ __launch_bounds__(kBlock) void bounce_kernel(DeviceScene sc, BounceAr
           s.ior = 1.00029f;
         }
       } else {
+        uint32_t lo = seg_lo, hi = seg_hi;   // last j with seg[j] <= idx
+        while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
+        const uint32_t slot = lo * in_chunk + (idx - seg[lo]);
         const float4 q0 = a.in_q.plane[0][slot], q1 = a.in_q.plane[1][slot];
         const float4 q2 = a.in_q.plane[2][slot], q3 = a.in_q.plane[3][slot];
         s.o = mk(q0);
@@ -616,34 +816,56 @@ __global__ __launch_bounds__(kBlock) void bounce_kernel(DeviceScene sc, BounceAr
         x = pix - y * a.width;
       }
     }
-    bool alive = false;
-    if (active) {
-      const Hit h = trace_nearest<STACK>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
-      if (!h.found || h.t < kDistanceEpsilon) {
-        accumulate_pixel(a.image, pix, s.R, a.frame_index);   // path terminated (Shaders.metal:122-126)
+    STAMP(0);
+    // -- phase 1: nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
+    Hit h;
+    h.found = false;
+    if (active) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+    STAMP(1);
+    // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
+    //    near hit ends the path (:122-126)
+    const bool hit_ok = active && h.found && !(h.t < kDistanceEpsilon);
+    ShadowRay sh;
+    sh.valid = false;
+    if (hit_ok) {
+      const float4 ns = a.noise_shade[shade_noise_cell(x, y, a.bounce, a.frame_index)];
+      if (a.debug & 2u) {   // ablation: no shading, reflect back along the ray
+        s.o = add(s.o, mul(s.d, h.t * 0.999f));
+        s.d = mk(-s.d.x, -s.d.y, -s.d.z);
       } else {
-        const float4 ns = a.noise_shade[shade_noise_cell(x, y, a.bounce, a.frame_index)];
-        ShadowRay sh;
-        shade_hit(sc, h, s, ns, a.bounce, a.max_path_length, !last, sh);
-        if (sh.valid && shadow_reaches_target<STACK>(sc, cx, sh.o, sh.d, sh.target)) s.R = add(s.R, sh.L);
-        if (last) accumulate_pixel(a.image, pix, s.R, a.frame_index);
-        else alive = true;
+        shade_hit<MODE>(sc, cx, h, s, ns, a.bounce, a.max_path_length, !last, sh);
       }
     }
-    // wave-level stream compaction of the survivors
+    STAMP(2);
+    // -- phase 3: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
+    if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target)))
+      s.R = add(s.R, sh.L);
+    STAMP(3);
+    // -- phase 4: finished paths accumulate (accumulateImage, :233-249);
+    //    survivors are compacted into this block's segment of the next queue
+    if (active && (!hit_ok || last)) accumulate_pixel(a.image, pix, s.R, a.frame_index);
+    const bool alive = hit_ok && !last;
     const uint64_t mask = __ballot(alive);
     if (mask) {
       uint32_t wbase = 0;
-      if (lane == 0) wbase = atomicAdd(a.out_count, (uint32_t)__popcll(mask));
+      if (lane == 0) wbase = atomicAdd(&s_cursor, (uint32_t)__popcll(mask));
       wbase = __shfl(wbase, 0);
-      if (alive) {
-        const uint32_t o = wbase + (uint32_t)__popcll(mask & lanes_below);
+      if (alive && !(a.debug & 4u)) {
+        const uint32_t o = out_base + wbase + (uint32_t)__popcll(mask & lanes_below);
         a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, s.pdf);
         a.out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, s.ior);
         a.out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, bitsf(pix | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
         a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
       }
     }
+    STAMP(4);
+  }
+  STAMP_FLUSH();
+  __syncthreads();
+  if (tid == 0) {
+    a.out_seg_count[blockIdx.x] = s_cursor;
+    if (s_cursor) atomicAdd(a.out_total, s_cursor);   // stats: one atomic per block per launch
+    if (blockIdx.x == 0) *a.out_chunk = chunk;
   }
 }
 
@@ -666,15 +888,14 @@ __global__ __launch_bounds__(kBlock) void raygen_kernel(uint32_t W, uint32_t H, 
 
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DeviceScene sc, const uint8_t* rays, uint32_t stride,
                                                            uint32_t count, RefIntersection* out) {
-  __shared__ uint32_t stack[kMaxStack * kBlock];
+  const LdsCtx cx = stage_lds<kGlobal>(sc, 0);
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= count) return;
-  TraversalCtx cx{nullptr, 0u, stack + threadIdx.x};
   const float* r = reinterpret_cast<const float*>(rays + (size_t)i * stride);
   RefIntersection res{-1.0f, 0xFFFFFFFFu, {0.0f, 0.0f}};
   const float tmax = r[7];
   if (tmax >= 0.0f) {   // maxDistance < 0 disables the ray (Shaders.metal:124,173)
-    const Hit h = trace_nearest<kMaxStack>(sc, cx, mk(r[0], r[1], r[2]), mk(r[4], r[5], r[6]), r[3], tmax);
+    const Hit h = trace_nearest<kMaxStack, kGlobal>(sc, cx, mk(r[0], r[1], r[2]), mk(r[4], r[5], r[6]), r[3], tmax);
     if (h.found) {
       res.distance = h.t;
       res.triangleIndex = h.prim;
@@ -709,7 +930,8 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DeviceScene sc, uint32_t 
   Hit h;
   h.t = is.distance; h.prim = is.triangleIndex; h.u = is.coordinates[0]; h.v = is.coordinates[1]; h.found = true;
   ShadowRay sh;
-  shade_hit(sc, h, s, noise[shade_noise_cell(x, y, bounce, f)], bounce, L, true, sh);
+  const LdsCtx cx = stage_lds<kGlobal>(sc, 0);
+  shade_hit<kGlobal>(sc, cx, h, s, noise[shade_noise_cell(x, y, bounce, f)], bounce, L, true, sh);
   if (bounce + 1 < L) {
     sr.origin[0] = sh.o.x; sr.origin[1] = sh.o.y; sr.origin[2] = sh.o.z;
     sr.direction[0] = sh.d.x; sr.direction[1] = sh.d.y; sr.direction[2] = sh.d.z;
@@ -744,31 +966,62 @@ __global__ __launch_bounds__(kBlock) void accumulate_kernel(uint32_t W, uint32_t
 
 inline uint32_t blocks_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 
-template <int STACK>
-hipError_t launch_bounce_t(const DeviceScene& sc, const BounceArgs& a, hipStream_t s) {
-  const size_t lds_bytes = (size_t)sc.lds_nodes * 64 + (size_t)STACK * kBlock * 4;
-  // occupancy-sized persistent grid, cached per (device, LDS footprint)
-  static int cached_dev = -1, blocks_per_cu = 1, cus = 0;
-  static size_t cached_lds = 0;
+constexpr size_t kAllLdsBudget = 48 * 1024;   // scene bytes staged whole in LDS
+
+int choose_mode(const DeviceScene& sc) {
+  if ((size_t)lds_scene_float4s(kAllLds, sc.num_nodes, 0, sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16 <=
+      kAllLdsBudget)
+    return kAllLds;
+  return sc.lds_nodes > 0 ? kTopLds : kGlobal;
+}
+
+size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
+  const size_t scene = (size_t)lds_scene_float4s(mode, sc.num_nodes, sc.lds_nodes, sc.num_triangles,
+                                                 sc.num_materials, sc.num_lights + 1) * 16;
+  const size_t scratch = ((size_t)grid + 1 + 3) / 4 * 16;
+  return scene + scratch + (size_t)stack * kBlock * 4;
+}
+
+template <int STACK, int MODE>
+hipError_t grid_for(const DeviceScene& sc, uint32_t* grid) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (dev != cached_dev || lds_bytes != cached_lds) {
-    hipDeviceProp_t prop;
-    e = hipGetDeviceProperties(&prop, dev);
-    if (e != hipSuccess) return e;
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bounce_kernel<STACK>, kBlock, lds_bytes) != hipSuccess || n <= 0)
-      n = 1;
-    cus = prop.multiProcessorCount;
-    blocks_per_cu = n;
-    cached_dev = dev;
-    cached_lds = lds_bytes;
-  }
-  uint32_t grid = (uint32_t)(cus * blocks_per_cu);
-  if (a.bounce == 0) grid = std::min<uint32_t>(grid, std::max<uint32_t>(1, blocks_for(a.num_slots)));
-  bounce_kernel<STACK><<<dim3(grid), dim3(kBlock), lds_bytes, s>>>(sc, a);
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return e;
+  // the scratch depends on the grid: size with the worst case (8 blocks/CU)
+  const size_t lds = bounce_lds_bytes(sc, MODE, STACK, (uint32_t)prop.multiProcessorCount * 8);
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bounce_kernel<STACK, MODE>, kBlock, lds) != hipSuccess || n <= 0)
+    n = 1;
+  *grid = (uint32_t)(prop.multiProcessorCount * std::min(n, 8));
+  return hipSuccess;
+}
+
+template <int STACK, int MODE>
+hipError_t launch_bounce_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
+  const size_t lds = bounce_lds_bytes(sc, MODE, STACK, grid);
+  bounce_kernel<STACK, MODE><<<dim3(grid), dim3(kBlock), lds, s>>>(sc, a);
   return hipGetLastError();
+}
+
+template <int STACK>
+hipError_t dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
+                         hipStream_t s) {
+  switch (choose_mode(sc)) {
+    case kAllLds: return a ? launch_bounce_t<STACK, kAllLds>(sc, *a, grid, s) : grid_for<STACK, kAllLds>(sc, grid_out);
+    case kTopLds: return a ? launch_bounce_t<STACK, kTopLds>(sc, *a, grid, s) : grid_for<STACK, kTopLds>(sc, grid_out);
+    default: return a ? launch_bounce_t<STACK, kGlobal>(sc, *a, grid, s) : grid_for<STACK, kGlobal>(sc, grid_out);
+  }
+}
+
+hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_entries, uint32_t grid,
+                    uint32_t* grid_out, hipStream_t s) {
+  if (stack_entries <= 8) return dispatch_mode<8>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 16) return dispatch_mode<16>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 24) return dispatch_mode<24>(sc, a, grid, grid_out, s);
+  return dispatch_mode<32>(sc, a, grid, grid_out, s);
 }
 
 }  // namespace
@@ -782,7 +1035,7 @@ hipError_t launch_raygen(uint32_t W, uint32_t H, const float* noise, RefRay* ray
 hipError_t launch_intersect(const DeviceScene& sc, const void* rays, uint32_t stride, uint32_t count,
                             RefIntersection* out, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  intersect_kernel<<<dim3(blocks_for(count)), dim3(kBlock), 0, s>>>(sc,
+  intersect_kernel<<<dim3(blocks_for(count)), dim3(kBlock), (size_t)kMaxStack * kBlock * 4, s>>>(sc,
                      reinterpret_cast<const uint8_t*>(rays), stride, count, out);
   return hipGetLastError();
 }
@@ -809,11 +1062,26 @@ hipError_t launch_accumulate(uint32_t W, uint32_t H, uint32_t frame_index, const
   return hipGetLastError();
 }
 
-hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, hipStream_t s) {
-  if (stack_entries <= 8) return launch_bounce_t<8>(sc, a, s);
-  if (stack_entries <= 16) return launch_bounce_t<16>(sc, a, s);
-  if (stack_entries <= 24) return launch_bounce_t<24>(sc, a, s);
-  return launch_bounce_t<32>(sc, a, s);
+hipError_t read_stamps(unsigned long long* out8, bool reset) {
+#if MRT_STAMPS
+  hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), 8 * sizeof(unsigned long long));
+  if (e != hipSuccess || !reset) return e;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+#else
+  (void)reset;
+  for (int k = 0; k < 8; ++k) out8[k] = 0;
+  return hipSuccess;
+#endif
+}
+
+hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid) {
+  return dispatch(sc, nullptr, stack_entries, 0, grid, nullptr);
+}
+
+hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,
+                         hipStream_t s) {
+  return dispatch(sc, &a, stack_entries, grid, nullptr, s);
 }
 
 }  // namespace MRT_NS

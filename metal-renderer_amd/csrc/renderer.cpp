@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -84,7 +85,9 @@ struct mrt_renderer {
   uint32_t tiles_x = 0, tiles_y = 0, owned_tiles = 0;
   uint64_t owned_pixels = 0;
   DevBuf queue[2][4];
-  DevBuf counters;
+  DevBuf counters;          // per (frame, bounce) survivor totals (stats)
+  DevBuf segments;          // 2 x grid per-block survivor counts + 2 chunk words
+  uint32_t grid = 0;        // persistent grid of the bounce kernel
   // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
   DevBuf noise_init, noise_window;
   int64_t noise_first = 0, noise_count = 0;
@@ -97,6 +100,7 @@ struct mrt_renderer {
   size_t pending_events = 0;
   mrt_stats stats{};
   uint32_t stack_entries = 32;
+  uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
 };
 
 namespace {
@@ -175,7 +179,10 @@ int alloc_frame_buffers(mrt_renderer* r) {
     const uint64_t h = std::min<uint32_t>(mrt::kTile, H - ty * mrt::kTile);
     r->owned_pixels += w * h;
   }
-  const size_t slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096);
+  // queue capacity: every owned slot + per-block rounding of the segments
+  const size_t slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096) + (size_t)r->grid * 256;
+  HIP_TRY(r->segments.alloc(((size_t)2 * r->grid + 2) * 4));
+  HIP_TRY(hipMemsetAsync(r->segments.p, 0, r->segments.bytes, r->stream));
   for (int q = 0; q < 2; ++q)
     for (int p = 0; p < 4; ++p) HIP_TRY(r->queue[q][p].alloc(slots * 16));
   if (r->own_image) {
@@ -191,8 +198,9 @@ int alloc_frame_buffers(mrt_renderer* r) {
 }
 
 inline hipError_t launch_bounce(const mrt_renderer* r, const mrt::BounceArgs& a) {
-  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_bounce(r->scene->dev, a, r->stack_entries, r->stream);
-  return mrt::fast::launch_bounce(r->scene->dev, a, r->stack_entries, r->stream);
+  if (r->desc.flags & MRT_FLAG_PRECISE)
+    return mrt::precise::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, r->stream);
+  return mrt::fast::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, r->stream);
 }
 
 bool precise(uint32_t flags) { return (flags & MRT_FLAG_PRECISE) != 0; }
@@ -283,6 +291,12 @@ int mrt_device_count(void) {
 int mrt_synchronize(void* stream) {
   if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   else HIP_TRY(hipDeviceSynchronize());
+  return MRT_OK;
+}
+
+int mrt_debug_stamps(uint64_t* out8, int reset) {
+  if (!out8) return fail(MRT_ERR_INVALID, "null output");
+  HIP_TRY(mrt::fast::read_stamps(reinterpret_cast<unsigned long long*>(out8), reset != 0));
   return MRT_OK;
 }
 
@@ -545,6 +559,10 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   HIP_TRY(hipEventCreate(&r->ev_stop));
   const uint32_t depth = desc->scene->bvh.max_depth;
   r->stack_entries = depth <= 8 ? 8 : depth <= 16 ? 16 : depth <= 24 ? 24 : 32;
+  if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
+  HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, &r->grid)
+                                           : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, &r->grid));
+  if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
   int rc = alloc_frame_buffers(r.get());
   if (rc) return rc;
   *out = r.release();
@@ -614,8 +632,15 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.shard_count = r->desc.shard_count;
       a.tiles_x = r->tiles_x;
       a.num_slots = r->owned_tiles * 4096u;
-      a.in_count = b ? cnt + (size_t)k * L + (b - 1) : nullptr;
-      a.out_count = cnt + (size_t)k * L + b;
+      a.debug = r->debug;
+      uint32_t* seg = r->segments.as<uint32_t>();
+      uint32_t* meta = seg + 2 * (size_t)r->grid;
+      a.in_segments = r->grid;
+      a.in_seg_count = seg + (size_t)((b + 1) & 1) * r->grid;
+      a.in_chunk = meta + ((b + 1) & 1);
+      a.out_seg_count = seg + (size_t)(b & 1) * r->grid;
+      a.out_chunk = meta + (b & 1);
+      a.out_total = cnt + (size_t)k * L + b;
       for (int p = 0; p < 4; ++p) {
         a.in_q.plane[p] = r->queue[b & 1][p].as<float4>();
         a.out_q.plane[p] = r->queue[(b + 1) & 1][p].as<float4>();

@@ -29,7 +29,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libmrt.so")
+LIB_PATH = os.environ.get("MRT_LIB") or os.path.join(HERE, "lib", "libmrt.so")   # MRT_LIB: diagnostic builds
 INCLUDE_H = os.path.join(os.path.dirname(HERE), "include", "mrt.h")
 SCENES_DIR = os.path.join(os.path.dirname(HERE), "tests", "golden", "scenes")
 
@@ -96,6 +96,7 @@ EXPORTED = [
     "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image",
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
+    "mrt_debug_stamps",
 ]
 
 _lib = None
@@ -142,6 +143,7 @@ def lib() -> ctypes.CDLL:
         "mrt_noise_table": [u64, i64, vp],
         "mrt_device_count": [],
         "mrt_synchronize": [vp],
+        "mrt_debug_stamps": [vp, c_int],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -338,6 +340,13 @@ def noise_table(seed: int, frame: int):
     import numpy as np
     out = np.zeros(64 * 64 * 4, np.float32)
     _check(lib().mrt_noise_table(seed, frame, ctypes.c_void_p(out.ctypes.data)), "mrt_noise_table")
+    return out
+
+
+def debug_stamps(reset: bool = True):
+    import numpy as np
+    out = np.zeros(8, np.uint64)
+    _check(lib().mrt_debug_stamps(ctypes.c_void_p(out.ctypes.data), int(reset)), "mrt_debug_stamps")
     return out
 
 
