@@ -166,6 +166,11 @@ int mrt_abi_version(void);
 /* The deterministic noise table of SURVEY.md A.3 for frame `frame` (-1 = the
  * initial table), 64*64*4 floats, host memory. */
 int mrt_noise_table(uint64_t seed, int64_t frame, float* out16384);
+/* Host helper (no device needed): the pixels a shard owns under the 64x64
+ * tile round-robin (tile t -> shard t % shard_count), as a W*H byte mask
+ * (row 0 = bottom); returns the number of owned pixels via *owned. */
+int mrt_shard_mask(uint32_t width, uint32_t height, uint32_t shard_rank, uint32_t shard_count, uint8_t* mask,
+                   uint64_t* owned);
 /* Wait for work queued by libmrt on `stream` (NULL = everything on the device
  * libmrt's runtime has queued). */
 int mrt_synchronize(void* stream);

@@ -14,10 +14,12 @@
 namespace mrt {
 
 // Ray queue: SoA of four float4 planes, one record per ray slot:
-//   plane 0: (origin.xyz, material pdf)          = Ray.origin, Ray.params.x
-//   plane 1: (direction.xyz, ior)                = Ray.direction, Ray.params.w
-//   plane 2: (throughput.rgb, bits(pixel | prevDiffuse << 31))
-//   plane 3: (radiance.rgb, 0)
+//   plane 0: (origin.xyz, bits(pixel | prevDiffuse << 31))   = Ray.origin, params.y
+//   plane 1: (direction.xyz, 0)                            = Ray.direction
+//   plane 2: (throughput.rgb, material pdf)                = Ray.throughput, params.x
+//   plane 3: (radiance.rgb, ior)                           = Ray.radiance, params.w
+// Planes 0-1 are all the traversal needs; planes 2-3 are loaded after the
+// hit so they do not occupy registers during traversal.
 // The bounce index (Ray.params.z) is uniform per launch and not stored.
 struct RayQueue {
   float4* plane[4];

@@ -26,6 +26,17 @@ namespace MRT_NS {
 namespace {
 
 constexpr int kBlock = 256;   // 4 waves of 64 lanes
+#ifndef MRT_SHADE_BARRIERS
+#define MRT_SHADE_BARRIERS 0
+#endif
+#if MRT_SHADE_BARRIERS
+#define MRT_SHADE_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define MRT_SHADE_BARRIER() do {} while (0)
+#endif
+#ifndef MRT_WHILE_WHILE
+#define MRT_WHILE_WHILE 0
+#endif
 #ifndef MRT_BOUNCE_WAVES
 #define MRT_BOUNCE_WAVES 1
 #endif
@@ -80,6 +91,8 @@ __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); 
 // interpolate() expects (renderer/KernelHelpers.h:37-47).
 __device__ __forceinline__ bool tri_test(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float tmin, float tmax, float& t,
                                          float& u, float& v) {
+  // early exits: most candidate triangles fail the first barycentric test,
+  // and a wave whose lanes all fail skips the rest (s_cbranch_execz)
   const V3 p = cross(d, e2);
   const float det = dot(e1, p);
   if (det == 0.0f) return false;
@@ -284,14 +297,20 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   return cx;
 }
 
-// Nearest hit in [tmin, tmax]; ties -> lowest primitive index.
-template <int STACK, int MODE>
-__device__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, float tmax) {
-  Hit h;
-  h.t = tmax;
-  h.u = h.v = 0.0f;
-  h.prim = 0xFFFFFFFFu;
-  h.found = false;
+// While-while traversal with postponed leaves (Aila & Laine 2009, recast for
+// 64-lane waves): a lane that reaches a leaf parks it and keeps descending
+// interior nodes until every lane of the wave holds a leaf, then the wave
+// tests leaves together — interior and leaf work are not interleaved lane by
+// lane.  The per-lane stack is in LDS; DONE marks an empty stack.
+// ANY = false: nearest hit in [tmin, h.t]; ties -> lowest primitive index.
+// ANY = true:  stop at the first primitive k != target with (t_k, k) <
+//              (t_target, target) in [0, t_target] (shadow occlusion).
+
+#if !MRT_WHILE_WHILE
+// "if-if" loop: one node or one leaf per iteration.
+template <int STACK, int MODE, bool ANY>
+__device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
+                                         uint32_t target) {
   const RayBox rb = make_raybox(o, d);
   int32_t node = sc.root;
   int sp = 0;
@@ -313,21 +332,22 @@ __device__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d
       if (hl) { node = rl; continue; }
       if (hr) { node = rr; continue; }
     } else {
-      const uint32_t leaf = ~(uint32_t)node;
-      const uint32_t first = leaf >> kLeafCountBits, cnt = (leaf & (kMaxLeafSize - 1)) + 1;
+      const uint32_t lr = ~(uint32_t)node;
+      const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
       for (uint32_t k = 0; k < cnt; ++k) {
         float4 t0, t1, t2;
         fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
+        const uint32_t prim = fbits(t0.w);
         float t, u, v;
-        if (tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v)) {
-          const uint32_t prim = fbits(t0.w);
-          if (!h.found || t < h.t || prim < h.prim) {
-            h.found = true;
-            h.t = t;
-            h.u = u;
-            h.v = v;
-            h.prim = prim;
-          }
+        const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v);
+        if (ANY) {
+          if (hit & (prim != target) & ((t < h.t) | (prim < target))) return true;
+        } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
+          h.found = true;
+          h.t = t;
+          h.u = u;
+          h.v = v;
+          h.prim = prim;
         }
       }
     }
@@ -335,52 +355,96 @@ __device__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d
     --sp;
     node = stack_get(cx, sp);
   }
-  return h;
+  return false;
 }
-
-// Is any primitive k != target hit with (t_k, k) < (t_target, target)?
-// (the shadow ray's MPS nearest hit is then not the target)
-template <int STACK, int MODE>
-__device__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                               float t_target) {
+#else
+constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
+template <int STACK, int MODE, bool ANY>
+__device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
+                                         uint32_t target) {
   const RayBox rb = make_raybox(o, d);
-  int32_t node = sc.root;
+  int32_t node = sc.root, leaf = 0;
   int sp = 0;
-  while (true) {
-    if (node >= 0) {
+  if (node < 0) { leaf = node; node = kDone; }
+  while (node != kDone || leaf != 0) {
+    // interior nodes
+    while (node != kDone && node >= 0) {
       float4 a, b, c, e;
       fetch_node<MODE>(sc, cx, node, a, b, c, e);
       bool hl, hr;
       float tnl, tnr;
-      box2(a, b, c, o, rb, 0.0f, t_target, hl, hr, tnl, tnr);
+      box2(a, b, c, o, rb, tmin, h.t, hl, hr, tnl, tnr);
       const int32_t rl = (int32_t)fbits(e.x), rr = (int32_t)fbits(e.y);
-      if (hl && hr) {
-        const bool swap = tnr < tnl;
-        const int32_t nearer = swap ? rr : rl, farther = swap ? rl : rr;
-        if (sp < STACK) { stack_push(cx, sp, farther); ++sp; }
-        node = nearer;
-        continue;
+      if (hl | hr) {
+        const bool right_first = !hl || (hr && tnr < tnl);
+        node = right_first ? rr : rl;
+        if (hl & hr) {
+          if (sp < STACK) stack_push(cx, sp, right_first ? rl : rr);
+          sp = min(sp + 1, STACK);
+        }
+      } else {
+        node = sp > 0 ? stack_get(cx, sp - 1) : kDone;
+        sp = max(sp - 1, 0);
       }
-      if (hl) { node = rl; continue; }
-      if (hr) { node = rr; continue; }
-    } else {
-      const uint32_t leaf = ~(uint32_t)node;
-      const uint32_t first = leaf >> kLeafCountBits, cnt = (leaf & (kMaxLeafSize - 1)) + 1;
+      if (node < 0 && leaf == 0) {   // park the leaf, keep descending
+        leaf = node;
+        node = sp > 0 ? stack_get(cx, sp - 1) : kDone;
+        sp = max(sp - 1, 0);
+      }
+      if (!__any(leaf == 0)) break;
+    }
+    // leaves
+    while (leaf < 0) {
+      const uint32_t lr = ~(uint32_t)leaf;
+      const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
       for (uint32_t k = 0; k < cnt; ++k) {
         float4 t0, t1, t2;
         fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
         const uint32_t prim = fbits(t0.w);
-        if (prim == target) continue;
         float t, u, v;
-        if (tri_test(o, d, mk(t0), mk(t1), mk(t2), 0.0f, t_target, t, u, v) && (t < t_target || prim < target))
-          return true;
+        const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v);
+        if (ANY) {
+          if (hit & (prim != target) & ((t < h.t) | (prim < target))) return true;
+        } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
+          h.found = true;
+          h.t = t;
+          h.u = u;
+          h.v = v;
+          h.prim = prim;
+        }
+      }
+      leaf = 0;
+      if (node < 0) {   // the next node is a leaf too: take it now
+        leaf = node;
+        node = sp > 0 ? stack_get(cx, sp - 1) : kDone;
+        sp = max(sp - 1, 0);
       }
     }
-    if (sp == 0) break;
-    --sp;
-    node = stack_get(cx, sp);
   }
   return false;
+}
+
+#endif
+
+template <int STACK, int MODE>
+__device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
+                                             float tmax) {
+  Hit h;
+  h.t = tmax;
+  h.u = h.v = 0.0f;
+  h.prim = 0xFFFFFFFFu;
+  h.found = false;
+  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u);
+  return h;
+}
+
+template <int STACK, int MODE>
+__device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
+                                               float t_target) {
+  Hit h;
+  h.t = t_target;
+  h.found = false;
+  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target);
 }
 
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
@@ -579,36 +643,58 @@ __device__ __forceinline__ uint32_t shade_noise_cell(uint32_t x, uint32_t y, uin
 template <int MODE>
 __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& cx, const Hit& h, PathState& s,
                                           const float4& ns, uint32_t bounce, uint32_t L, bool next, ShadowRay& sh) {
-  const float4 P0 = fetch_prim<MODE>(sc, cx, h.prim, 0), P1 = fetch_prim<MODE>(sc, cx, h.prim, 1);
-  const float4 P2 = fetch_prim<MODE>(sc, cx, h.prim, 2), N0 = fetch_prim<MODE>(sc, cx, h.prim, 3);
-  const float4 N1 = fetch_prim<MODE>(sc, cx, h.prim, 4), N2 = fetch_prim<MODE>(sc, cx, h.prim, 5);
-  const uint32_t mat_index = fbits(P0.w);
-  const uint32_t light_index = fbits(P1.w);
-  const Mat m = load_material<MODE>(sc, cx, mat_index);
+  // Loads are staged behind scheduling barriers: hoisting all 13 float4
+  // record loads together would pin ~50 VGPRs and halve occupancy.
   // interpolate(float2) — KernelHelpers.h:23-47
   const float wu = h.u, wv = h.v, ww = (1.0f - h.u) - h.v;
-  const V3 hv = add(add(mul(mk(P0), wu), mul(mk(P1), wv)), mul(mk(P2), ww));
-  const V3 hn = normalize(add(add(mul(mk(N0), wu), mul(mk(N1), wv)), mul(mk(N2), ww)));
+  uint32_t mat_index, light_index;
+  V3 hv, hn;
+  {
+    const float4 P0 = fetch_prim<MODE>(sc, cx, h.prim, 0), P1 = fetch_prim<MODE>(sc, cx, h.prim, 1);
+    const float4 P2 = fetch_prim<MODE>(sc, cx, h.prim, 2);
+    mat_index = fbits(P0.w);
+    light_index = fbits(P1.w);
+    hv = add(add(mul(mk(P0), wu), mul(mk(P1), wv)), mul(mk(P2), ww));
+  }
+  MRT_SHADE_BARRIER();
+  {
+    const float4 N0 = fetch_prim<MODE>(sc, cx, h.prim, 3), N1 = fetch_prim<MODE>(sc, cx, h.prim, 4);
+    const float4 N2 = fetch_prim<MODE>(sc, cx, h.prim, 5);
+    hn = normalize(add(add(mul(mk(N0), wu), mul(mk(N1), wv)), mul(mk(N2), ww)));
+  }
+  MRT_SHADE_BARRIER();
+  const Mat m = load_material<MODE>(sc, cx, mat_index);
   const V3 wI = s.d;
   sh.valid = false;
   // light sampling — Shaders.metal:150-176
   if (bounce + 1 < L) {
     const uint32_t li = selectLightTriangle<MODE>(sc, cx, sc.num_lights, ns.z);
-    const float4 LA = fetch_light<MODE>(sc, cx, li, 0), LB = fetch_light<MODE>(sc, cx, li, 1);
-    const float4 LC = fetch_light<MODE>(sc, cx, li, 2), LD = fetch_light<MODE>(sc, cx, li, 3);
-    const float4 LE = fetch_light<MODE>(sc, cx, li, 4), LF = fetch_light<MODE>(sc, cx, li, 5);
-    const float4 LG = fetch_light<MODE>(sc, cx, li, 6);
     // barycentric(noise.wx) — Raytracing.h:182-187
     const float r1 = m_sqrt(ns.w), r2 = ns.x;
     const float bu = 1.0f - r1, bv = r1 * (1.0f - r2), bw = r1 * r2;
-    const V3 lv = add(add(mul(mk(LB), bu), mul(mk(LD), bv)), mul(mk(LF), bw));
-    const V3 ln = normalize(add(add(mul(mk(LC), bu), mul(mk(LE), bv)), mul(mk(LG), bw)));
+    V3 lv, ln;
+    float lpdf;
+    uint32_t lindex;
+    {
+      const float4 LB = fetch_light<MODE>(sc, cx, li, 1), LD = fetch_light<MODE>(sc, cx, li, 3);
+      const float4 LF = fetch_light<MODE>(sc, cx, li, 5);
+      lv = add(add(mul(mk(LB), bu), mul(mk(LD), bv)), mul(mk(LF), bw));
+      lpdf = LB.w;
+      lindex = fbits(LD.w);
+    }
+    MRT_SHADE_BARRIER();
+    {
+      const float4 LC = fetch_light<MODE>(sc, cx, li, 2), LE = fetch_light<MODE>(sc, cx, li, 4);
+      const float4 LG = fetch_light<MODE>(sc, cx, li, 6);
+      ln = normalize(add(add(mul(mk(LC), bu), mul(mk(LE), bv)), mul(mk(LG), bw)));
+    }
+    MRT_SHADE_BARRIER();
+    const float4 LA = fetch_light<MODE>(sc, cx, li, 0);
     V3 dirToLight;
-    const float lightPdf = lightTriangleSamplePDF(LB.w, LA.w, hv, lv, ln, dirToLight);
+    const float lightPdf = lightTriangleSamplePDF(lpdf, LA.w, hv, lv, ln, dirToLight);
     float materialBsdf, materialPdf;
     sampleMaterial(m, wI, dirToLight, hn, ns, materialBsdf, materialPdf);
     const float weight = balanceHeuristic(lightPdf, materialPdf);
-    const uint32_t lindex = fbits(LD.w);
     const float scale = m_div(weight * materialBsdf, lightPdf);
     sh.L = mk(((LA.x * m.kd.x) * s.T.x) * scale, ((LA.y * m.kd.y) * s.T.y) * scale,
               ((LA.z * m.kd.z) * s.T.z) * scale);
@@ -772,11 +858,11 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   STAMP_DECL();
   for (uint32_t base = begin + (tid & ~63u); base < end; base += kBlock) {
     STAMP_BEGIN();
-    // -- phase 0: generate (bounce 0) or load (SoA queue) the ray state
+    // -- phase 0: generate (bounce 0) or load (SoA queue planes 0-1) the ray
     const uint32_t idx = base + lane;
     bool active = idx < end;
     PathState s;
-    uint32_t pix = 0, x = 0, y = 0;
+    uint32_t tag = 0, slot = 0;   // tag = pixel | prevDiffuse << 31
     if (active) {
       if (a.bounce == 0) {
         // owned tile k -> global tile rank + k*count; 8x8 pixel blocks per wave
@@ -784,36 +870,28 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
         const uint32_t t = a.shard_rank + k * a.shard_count;
         const uint32_t tx = t % a.tiles_x, ty = t / a.tiles_x;
         const uint32_t blk = p >> 6, q = p & 63u;
-        x = tx * kTile + (blk & 7u) * 8u + (q & 7u);
-        y = ty * kTile + (blk >> 3) * 8u + (q >> 3);
+        const uint32_t x = tx * kTile + (blk & 7u) * 8u + (q & 7u);
+        const uint32_t y = ty * kTile + (blk >> 3) * 8u + (q >> 3);
         active = (x < a.width) && (y < a.height);
         if (active) {
-          pix = y * a.width + x;
+          tag = y * a.width + x;
           const float4 ns = a.noise_raygen[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
           camera_ray(x, y, a.width, a.height, ns, s.o, s.d);
-          s.T = mk(1.0f, 1.0f, 1.0f);
-          s.R = mk(0.0f, 0.0f, 0.0f);
-          s.pdf = 1.0f;
-          s.prevDiffuse = 0.0f;
-          s.ior = 1.00029f;
         }
       } else {
         uint32_t lo = seg_lo, hi = seg_hi;   // last j with seg[j] <= idx
         while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
-        const uint32_t slot = lo * in_chunk + (idx - seg[lo]);
+        slot = lo * in_chunk + (idx - seg[lo]);
         const float4 q0 = a.in_q.plane[0][slot], q1 = a.in_q.plane[1][slot];
         const float4 q2 = a.in_q.plane[2][slot], q3 = a.in_q.plane[3][slot];
         s.o = mk(q0);
-        s.pdf = q0.w;
+        tag = fbits(q0.w);
         s.d = mk(q1);
-        s.ior = q1.w;
         s.T = mk(q2);
-        const uint32_t tag = fbits(q2.w);
-        pix = tag & 0x7FFFFFFFu;
-        s.prevDiffuse = (tag >> 31) ? 1.0f : 0.0f;
+        s.pdf = q2.w;
         s.R = mk(q3);
-        y = pix / a.width;
-        x = pix - y * a.width;
+        s.ior = q3.w;
+        s.prevDiffuse = (tag >> 31) ? 1.0f : 0.0f;
       }
     }
     STAMP(0);
@@ -824,10 +902,19 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     STAMP(1);
     // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
     //    near hit ends the path (:122-126)
+    const uint32_t pix = tag & 0x7FFFFFFFu;
+    if (active && a.bounce == 0) {
+      s.T = mk(1.0f, 1.0f, 1.0f);
+      s.R = mk(0.0f, 0.0f, 0.0f);
+      s.pdf = 1.0f;
+      s.prevDiffuse = 0.0f;
+      s.ior = 1.00029f;
+    }
     const bool hit_ok = active && h.found && !(h.t < kDistanceEpsilon);
     ShadowRay sh;
     sh.valid = false;
     if (hit_ok) {
+      const uint32_t y = pix / a.width, x = pix - y * a.width;
       const float4 ns = a.noise_shade[shade_noise_cell(x, y, a.bounce, a.frame_index)];
       if (a.debug & 2u) {   // ablation: no shading, reflect back along the ray
         s.o = add(s.o, mul(s.d, h.t * 0.999f));
@@ -852,10 +939,10 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
       wbase = __shfl(wbase, 0);
       if (alive && !(a.debug & 4u)) {
         const uint32_t o = out_base + wbase + (uint32_t)__popcll(mask & lanes_below);
-        a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, s.pdf);
-        a.out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, s.ior);
-        a.out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, bitsf(pix | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
-        a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
+        a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(pix | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
+        a.out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
+        a.out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
+        a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
       }
     }
     STAMP(4);

@@ -288,6 +288,24 @@ int mrt_device_count(void) {
   return n;
 }
 
+int mrt_shard_mask(uint32_t W, uint32_t H, uint32_t rank, uint32_t count, uint8_t* mask, uint64_t* owned) {
+  if (W == 0 || H == 0) return fail(MRT_ERR_INVALID, "empty image");
+  const uint32_t S = count ? count : 1;
+  if (rank >= S) return fail(MRT_ERR_INVALID, "shard_rank >= shard_count");
+  const uint32_t tx_n = (W + mrt::kTile - 1) / mrt::kTile, ty_n = (H + mrt::kTile - 1) / mrt::kTile;
+  uint64_t n = 0;
+  for (uint32_t y = 0; y < H; ++y)
+    for (uint32_t x = 0; x < W; ++x) {
+      const uint32_t t = (y / mrt::kTile) * tx_n + x / mrt::kTile;
+      const bool mine = (t % S) == rank;
+      if (mask) mask[(size_t)y * W + x] = mine ? 1 : 0;
+      n += mine;
+    }
+  (void)ty_n;
+  if (owned) *owned = n;
+  return MRT_OK;
+}
+
 int mrt_synchronize(void* stream) {
   if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   else HIP_TRY(hipDeviceSynchronize());
@@ -327,6 +345,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (desc->lds_nodes == UINT32_MAX) opt.lds_node_budget = 0;
   else if (desc->lds_nodes) opt.lds_node_budget = desc->lds_nodes;
   else opt.lds_node_budget = 128;
+  // tuning overrides (profiling): MRT_LEAF = max leaf size, MRT_CTRAV = SAH node cost
+  if (const char* v = std::getenv("MRT_LEAF")) opt.max_leaf_size = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (const char* v = std::getenv("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
   const auto t0 = std::chrono::steady_clock::now();
   if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), h.indices.data(), T, opt, s->bvh, err))
     return fail(MRT_ERR_INVALID, "BVH build failed: " + err);

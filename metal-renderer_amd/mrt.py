@@ -96,7 +96,7 @@ EXPORTED = [
     "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image",
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
-    "mrt_debug_stamps",
+    "mrt_debug_stamps", "mrt_shard_mask",
 ]
 
 _lib = None
@@ -144,6 +144,7 @@ def lib() -> ctypes.CDLL:
         "mrt_device_count": [],
         "mrt_synchronize": [vp],
         "mrt_debug_stamps": [vp, c_int],
+        "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -341,6 +342,16 @@ def noise_table(seed: int, frame: int):
     out = np.zeros(64 * 64 * 4, np.float32)
     _check(lib().mrt_noise_table(seed, frame, ctypes.c_void_p(out.ctypes.data)), "mrt_noise_table")
     return out
+
+
+def shard_mask(width: int, height: int, rank: int, count: int):
+    """[H, W] uint8 ownership mask of a shard (row 0 = bottom) and its pixel count."""
+    import numpy as np
+    m = np.zeros((height, width), np.uint8)
+    n = np.zeros(1, np.uint64)
+    _check(lib().mrt_shard_mask(width, height, rank, count, ctypes.c_void_p(m.ctypes.data),
+                                ctypes.c_void_p(n.ctypes.data)), "mrt_shard_mask")
+    return m, int(n[0])
 
 
 def debug_stamps(reset: bool = True):
