@@ -45,7 +45,18 @@ struct BounceArgs {
   RayQueue in_q, out_q;
   const float4* noise_raygen;  // slot f%3  = T_f
   const float4* noise_shade;   // slot (f+i)%3
-  float4* image;               // RGBA32F accumulation image (row 0 = bottom)
+  float4* radiance;            // per-frame path radiance, written once per owned pixel when
+                               // its path ends (accumulated afterwards by launch_accumulate_frame)
+};
+
+// running-mean accumulation of one frame over the owned tiles
+struct AccumArgs {
+  uint32_t width, height;
+  uint32_t frame_index;
+  uint32_t shard_rank, shard_count, tiles_x;
+  uint32_t num_slots;          // owned tiles * 4096
+  const float4* radiance;
+  float4* image;
 };
 
 #define MRT_DECLARE_LAUNCHERS(NS)                                                                         \
@@ -65,6 +76,8 @@ struct BounceArgs {
   /* fused wavefront bounce over `grid` blocks (the same grid for every launch of a renderer) */          \
   hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
                            uint32_t grid, hipStream_t s);                                                 \
+  /* accumulateImage over the owned tiles of one frame (in frame order) */                                 \
+  hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s);                                  \
   /* diagnostic phase stamps (MRT_STAMPS builds; zeros otherwise) */                                      \
   hipError_t read_stamps(unsigned long long* out8, bool reset);                                          \
   }

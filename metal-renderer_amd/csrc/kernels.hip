@@ -34,6 +34,9 @@ constexpr int kBlock = 256;   // 4 waves of 64 lanes
 #else
 #define MRT_SHADE_BARRIER() do {} while (0)
 #endif
+#ifndef MRT_WAVE_TRAVERSAL
+#define MRT_WAVE_TRAVERSAL 1
+#endif
 #ifndef MRT_WHILE_WHILE
 #define MRT_WHILE_WHILE 0
 #endif
@@ -445,6 +448,113 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
   h.t = t_target;
   h.found = false;
   return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target);
+}
+
+// Wave-coherent ("packet") traversal for small scenes (kAllLds).  The whole
+// 64-lane wave walks the BVH together: node and triangle addresses are
+// wave-uniform (LDS broadcast reads, no bank conflicts, uniform branches), the
+// wave descends into a child when ANY live lane's box test passes, and one
+// wave-uniform stack (the lane-0 column of the per-lane stack) holds deferred
+// children.  Every lane tests a superset of the triangles its own traversal
+// would reach, with the same acceptance rule, so each lane's nearest hit is
+// exactly the per-lane (and brute-force) result.  Must be called by every
+// lane of the wave; `enabled` masks lanes without a ray.
+template <int STACK, int MODE, bool ANY>
+__device__ __forceinline__ bool traverse_wave(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
+                                              uint32_t target, bool enabled) {
+  const RayBox rb = make_raybox(o, d);
+  const uint32_t wstack = cx.stack_base - (threadIdx.x & 63u);   // lane-0 column of this wave
+  bool live = enabled;
+  bool occluded = false;
+  if (!__any(live)) return false;
+  int32_t node = sc.root;
+  int sp = 0;
+  while (true) {
+    if (node >= 0) {
+      float4 a, b, c, e;
+      fetch_node<MODE>(sc, cx, node, a, b, c, e);
+      bool hl, hr;
+      float tnl, tnr;
+      box2(a, b, c, o, rb, tmin, h.t, hl, hr, tnl, tnr);
+      hl = hl & live;
+      hr = hr & live;
+      const uint64_t ml = __ballot(hl), mr = __ballot(hr);
+      const int32_t rl = __builtin_amdgcn_readfirstlane((int32_t)fbits(e.x));
+      const int32_t rr = __builtin_amdgcn_readfirstlane((int32_t)fbits(e.y));
+      if (ml | mr) {
+        // majority vote on the nearer child among the lanes that hit one
+        const uint64_t pl = __ballot(hl & (!hr | (tnl <= tnr)));
+        const bool left_first = ml && (!mr || 2 * __popcll(pl) >= __popcll(ml | mr));
+        if (ml && mr) {
+          if (sp < STACK) lds_u32()[wstack + sp * kBlock] = (uint32_t)(left_first ? rr : rl);
+          sp = min(sp + 1, STACK);
+        }
+        node = left_first ? rl : rr;
+        continue;
+      }
+    } else {
+      const uint32_t lr = ~(uint32_t)node;
+      const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        float4 t0, t1, t2;
+        fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
+        const uint32_t prim = __builtin_amdgcn_readfirstlane(fbits(t0.w));
+        if (live) {
+          float t, u, v;
+          if (tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v)) {
+            if (ANY) {
+              if (prim != target && (t < h.t || prim < target)) {
+                occluded = true;
+                live = false;
+              }
+            } else if (!h.found || t < h.t || prim < h.prim) {
+              h.found = true;
+              h.t = t;
+              h.u = u;
+              h.v = v;
+              h.prim = prim;
+            }
+          }
+        }
+      }
+      if (ANY && !__any(live)) break;
+    }
+    if (sp == 0) break;
+    --sp;
+    node = __builtin_amdgcn_readfirstlane((int32_t)lds_u32()[wstack + sp * kBlock]);
+  }
+  return occluded;
+}
+
+template <int STACK, int MODE>
+__device__ __forceinline__ Hit trace_nearest_wave(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
+                                                  float tmax, bool enabled) {
+  Hit h;
+  h.t = tmax;
+  h.u = h.v = 0.0f;
+  h.prim = 0xFFFFFFFFu;
+  h.found = false;
+  traverse_wave<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u, enabled);
+  return h;
+}
+
+// Shadow visibility, wave-coherent form of shadow_reaches_target (below).
+template <int STACK, int MODE>
+__device__ __forceinline__ bool shadow_reaches_target_wave(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d,
+                                                           uint32_t target, bool enabled) {
+  float tT = 0.0f;
+  bool ok = false;
+  if (enabled) {
+    const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
+    const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
+    float u, v;
+    ok = tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) && (tT >= kDistanceEpsilon);
+  }
+  Hit h;
+  h.t = tT;
+  h.found = false;
+  const bool occ = traverse_wave<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, ok);
+  return ok && !occ;
 }
 
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
@@ -898,7 +1008,8 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     // -- phase 1: nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
     Hit h;
     h.found = false;
-    if (active) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+    if (MRT_WAVE_TRAVERSAL && MODE == kAllLds) h = trace_nearest_wave<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff(), active);
+    else if (active) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
     STAMP(1);
     // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
     //    near hit ends the path (:122-126)
@@ -925,12 +1036,16 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     }
     STAMP(2);
     // -- phase 3: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
-    if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target)))
+    if (MRT_WAVE_TRAVERSAL && MODE == kAllLds) {
+      const bool vis = (a.debug & 1u) ? sh.valid : shadow_reaches_target_wave<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target, sh.valid);
+      if (vis) s.R = add(s.R, sh.L);
+    } else if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target))) {
       s.R = add(s.R, sh.L);
+    }
     STAMP(3);
     // -- phase 4: finished paths accumulate (accumulateImage, :233-249);
     //    survivors are compacted into this block's segment of the next queue
-    if (active && (!hit_ok || last)) accumulate_pixel(a.image, pix, s.R, a.frame_index);
+    if (active && (!hit_ok || last)) a.radiance[pix] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
     const bool alive = hit_ok && !last;
     const uint64_t mask = __ballot(alive);
     if (mask) {
@@ -953,6 +1068,23 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     a.out_seg_count[blockIdx.x] = s_cursor;
     if (s_cursor) atomicAdd(a.out_total, s_cursor);   // stats: one atomic per block per launch
     if (blockIdx.x == 0) *a.out_chunk = chunk;
+  }
+}
+
+// accumulateImage (renderer/Shaders.metal:233-249) for one frame over the
+// owned tiles: image = f == 0 ? c : mix(c, image, f/(f+1)).  Frames are
+// accumulated strictly in order (the running mean is order-dependent).
+__global__ __launch_bounds__(kBlock) void accumulate_frame_kernel(AccumArgs a) {
+  for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < a.num_slots; idx += gridDim.x * kBlock) {
+    const uint32_t k = idx >> 12, p = idx & 4095u;
+    const uint32_t t = a.shard_rank + k * a.shard_count;
+    const uint32_t tx = t % a.tiles_x, ty = t / a.tiles_x;
+    // row-major inside the tile: consecutive lanes -> consecutive pixels
+    const uint32_t x = tx * kTile + (p & 63u), y = ty * kTile + (p >> 6);
+    if (x >= a.width || y >= a.height) continue;
+    const uint32_t pix = y * a.width + x;
+    const float4 c = a.radiance[pix];
+    accumulate_pixel(a.image, pix, mk(c), a.frame_index);
   }
 }
 
@@ -1146,6 +1278,12 @@ hipError_t launch_accumulate(uint32_t W, uint32_t H, uint32_t frame_index, const
                              hipStream_t s) {
   accumulate_kernel<<<dim3(blocks_for(W * H)), dim3(kBlock), 0, s>>>(W, H, frame_index, rays,
                      reinterpret_cast<float4*>(image));
+  return hipGetLastError();
+}
+
+hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s) {
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks_for(a.num_slots), 4096));
+  accumulate_frame_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(a);
   return hipGetLastError();
 }
 

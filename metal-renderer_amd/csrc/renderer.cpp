@@ -75,18 +75,32 @@ struct mrt_scene {
   mrt_scene_info info{};
 };
 
+// One in-flight frame: its queues, segment counts, per-pixel path radiance and
+// the stream its bounce launches run on.  Frames f and f+1 run on different
+// slots concurrently (the reference keeps up to 3 frames in flight,
+// renderer/Renderer.mm:16,593-600); their accumulations are chained in frame
+// order with events because the running mean is order-dependent.
+struct FrameSlot {
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  DevBuf queue[2][4];
+  DevBuf segments;          // 2 x grid per-block survivor counts + 2 chunk words
+  DevBuf radiance;          // W*H float4, written once per owned pixel per frame
+  hipEvent_t acc_done = nullptr;
+};
+
 struct mrt_renderer {
   const mrt_scene* scene = nullptr;
   mrt_renderer_desc desc{};
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // main stream (external or own); slot 0 runs on it
   bool own_stream = false;
   float* image = nullptr;
   bool own_image = false;
   uint32_t tiles_x = 0, tiles_y = 0, owned_tiles = 0;
   uint64_t owned_pixels = 0;
-  DevBuf queue[2][4];
+  std::vector<FrameSlot> slots;
+  uint32_t inflight = 2;
   DevBuf counters;          // per (frame, bounce) survivor totals (stats)
-  DevBuf segments;          // 2 x grid per-block survivor counts + 2 chunk words
   uint32_t grid = 0;        // persistent grid of the bounce kernel
   // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
   DevBuf noise_init, noise_window;
@@ -181,10 +195,13 @@ int alloc_frame_buffers(mrt_renderer* r) {
   }
   // queue capacity: every owned slot + per-block rounding of the segments
   const size_t slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096) + (size_t)r->grid * 256;
-  HIP_TRY(r->segments.alloc(((size_t)2 * r->grid + 2) * 4));
-  HIP_TRY(hipMemsetAsync(r->segments.p, 0, r->segments.bytes, r->stream));
-  for (int q = 0; q < 2; ++q)
-    for (int p = 0; p < 4; ++p) HIP_TRY(r->queue[q][p].alloc(slots * 16));
+  for (FrameSlot& fs : r->slots) {
+    HIP_TRY(fs.segments.alloc(((size_t)2 * r->grid + 2) * 4));
+    HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
+    for (int q = 0; q < 2; ++q)
+      for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(slots * 16));
+    HIP_TRY(fs.radiance.alloc((size_t)W * H * 16));
+  }
   if (r->own_image) {
     if (r->image) (void)hipFree(r->image);
     r->image = nullptr;
@@ -197,10 +214,14 @@ int alloc_frame_buffers(mrt_renderer* r) {
   return MRT_OK;
 }
 
-inline hipError_t launch_bounce(const mrt_renderer* r, const mrt::BounceArgs& a) {
-  if (r->desc.flags & MRT_FLAG_PRECISE)
-    return mrt::precise::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, r->stream);
-  return mrt::fast::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, r->stream);
+inline hipError_t launch_bounce(const mrt_renderer* r, const mrt::BounceArgs& a, hipStream_t s) {
+  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, s);
+  return mrt::fast::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, s);
+}
+
+inline hipError_t launch_accumulate_frame(const mrt_renderer* r, const mrt::AccumArgs& a, hipStream_t s) {
+  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_accumulate_frame(a, s);
+  return mrt::fast::launch_accumulate_frame(a, s);
 }
 
 bool precise(uint32_t flags) { return (flags & MRT_FLAG_PRECISE) != 0; }
@@ -581,6 +602,19 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   const uint32_t depth = desc->scene->bvh.max_depth;
   r->stack_entries = depth <= 8 ? 8 : depth <= 16 ? 16 : depth <= 24 ? 24 : 32;
   if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
+  if (const char* v = std::getenv("MRT_INFLIGHT")) r->inflight = (uint32_t)std::strtoul(v, nullptr, 0);
+  r->inflight = std::max<uint32_t>(1, std::min<uint32_t>(3, r->inflight));
+  r->slots.resize(r->inflight);
+  for (uint32_t k = 0; k < r->inflight; ++k) {
+    FrameSlot& fs = r->slots[k];
+    if (k == 0) {
+      fs.stream = r->stream;
+    } else {
+      HIP_TRY(hipStreamCreateWithFlags(&fs.stream, hipStreamNonBlocking));
+      fs.own_stream = true;
+    }
+    HIP_TRY(hipEventCreateWithFlags(&fs.acc_done, hipEventDisableTiming));
+  }
   HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, &r->grid)
                                            : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, &r->grid));
   if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
@@ -638,10 +672,15 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     }
   }
   HIP_TRY(hipEventRecord(r->ev_start, r->stream));
+  for (uint32_t k = 1; k < r->inflight; ++k) HIP_TRY(hipStreamWaitEvent(r->slots[k].stream, r->ev_start, 0));
   uint32_t* cnt = r->counters.as<uint32_t>();
   size_t ev = 0;
+  const FrameSlot* prev = nullptr;
   for (uint32_t k = 0; k < n; ++k) {
     const uint64_t f = r->frame_index + k;
+    FrameSlot& fs = r->slots[k % r->inflight];
+    uint32_t* seg = fs.segments.as<uint32_t>();
+    uint32_t* meta = seg + 2 * (size_t)r->grid;
     for (uint32_t b = 0; b < L; ++b) {
       mrt::BounceArgs a{};
       a.width = r->desc.width;
@@ -654,8 +693,6 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.tiles_x = r->tiles_x;
       a.num_slots = r->owned_tiles * 4096u;
       a.debug = r->debug;
-      uint32_t* seg = r->segments.as<uint32_t>();
-      uint32_t* meta = seg + 2 * (size_t)r->grid;
       a.in_segments = r->grid;
       a.in_seg_count = seg + (size_t)((b + 1) & 1) * r->grid;
       a.in_chunk = meta + ((b + 1) & 1);
@@ -663,17 +700,34 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.out_chunk = meta + (b & 1);
       a.out_total = cnt + (size_t)k * L + b;
       for (int p = 0; p < 4; ++p) {
-        a.in_q.plane[p] = r->queue[b & 1][p].as<float4>();
-        a.out_q.plane[p] = r->queue[(b + 1) & 1][p].as<float4>();
+        a.in_q.plane[p] = fs.queue[b & 1][p].as<float4>();
+        a.out_q.plane[p] = fs.queue[(b + 1) & 1][p].as<float4>();
       }
       a.noise_raygen = reinterpret_cast<const float4*>(noise_ptr(r, (int64_t)f));
       a.noise_shade = reinterpret_cast<const float4*>(noise_ptr(r, mrt::noise_frame_for_iteration((int64_t)f, b)));
-      a.image = reinterpret_cast<float4*>(r->image);
-      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], r->stream));
-      HIP_TRY(launch_bounce(r, a));
-      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], r->stream));
+      a.radiance = fs.radiance.as<float4>();
+      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
+      HIP_TRY(launch_bounce(r, a, fs.stream));
+      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
     }
+    // accumulateImage for frame f, after frame f-1's (running mean order)
+    if (prev && prev != &fs) HIP_TRY(hipStreamWaitEvent(fs.stream, prev->acc_done, 0));
+    mrt::AccumArgs acc{};
+    acc.width = r->desc.width;
+    acc.height = r->desc.height;
+    acc.frame_index = (uint32_t)f;
+    acc.shard_rank = r->desc.shard_rank;
+    acc.shard_count = r->desc.shard_count;
+    acc.tiles_x = r->tiles_x;
+    acc.num_slots = r->owned_tiles * 4096u;
+    acc.radiance = fs.radiance.as<float4>();
+    acc.image = reinterpret_cast<float4*>(r->image);
+    HIP_TRY(launch_accumulate_frame(r, acc, fs.stream));
+    HIP_TRY(hipEventRecord(fs.acc_done, fs.stream));
+    prev = &fs;
   }
+  // join every slot back into the main stream
+  for (uint32_t k = 1; k < r->inflight && k < n; ++k) HIP_TRY(hipStreamWaitEvent(r->stream, r->slots[k].acc_done, 0));
   HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
   r->pending = true;
   r->pending_frames = n;
@@ -736,6 +790,11 @@ int mrt_renderer_destroy(mrt_renderer* r) {
   (void)finalize_pending(r);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->own_image && r->image) (void)hipFree(r->image);
+  for (FrameSlot& fs : r->slots) {
+    if (fs.acc_done) (void)hipEventDestroy(fs.acc_done);
+    if (fs.own_stream) (void)hipStreamDestroy(fs.stream);
+  }
+  r->slots.clear();
   for (hipEvent_t e : r->kernel_events) (void)hipEventDestroy(e);
   if (r->ev_start) (void)hipEventDestroy(r->ev_start);
   if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
