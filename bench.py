@@ -136,16 +136,22 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_paths / elapsed / 1e6
 
-    # roofline of the dominant kernel (the fused bounce kernel; every launch of
+    # roofline of the dominant kernel (the fused bounce kernel: every launch of
     # the frame is one) from HIP events recorded around each launch on the
-    # renderer's stream, over the timed steps of this rank
+    # stream it runs on, over the timed steps of this rank.  With frames in
+    # flight the launches overlap, so two rates are reported:
+    #   achieved       = algorithmic bytes per launch / average launch duration
+    #                    (the definition rocprofv3's per-dispatch average checks)
+    #   achieved_busy  = algorithmic bytes / union of the launch intervals
     A = st["active_ray_bounces"] - base["active_ray_bounces"]
     P = st["paths"] - base["paths"]
     launches = st["kernel_launches"] - base["kernel_launches"]
     kms = st["kernel_ms"] - base["kernel_ms"]
+    busy_ms = st["kernel_busy_ms"] - base["kernel_busy_ms"]
     bytes_alg = B_PATH * P + B_BOUNCE * A
     avg_launch_ms = kms / max(1, launches)
     achieved = (bytes_alg / max(1, launches)) / (avg_launch_ms * 1e-3) / 1e9 if launches else 0.0
+    achieved_busy = bytes_alg / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
     traffic = None
     pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
     if os.path.exists(pmc_path):
@@ -172,6 +178,8 @@ def main():
                    "build": "precise" if args.precise else "fast"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "achieved_busy": round(achieved_busy, 1), "frac_busy": round(achieved_busy / HBM_PEAK_GBS, 4),
+                     "busy_ms_per_step": round(busy_ms / max(1, args.steps), 3),
                      "kernel": "bounce_kernel", "launches": launches, "avg_launch_ms": round(avg_launch_ms, 4),
                      "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
                      "active_ray_bounces_per_step": int(A / max(1, args.steps))},

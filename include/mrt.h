@@ -132,8 +132,10 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
   double last_draw_ms;             /* GPU time of the last draw/draw_n (HIP events) */
   double mpaths_per_s;             /* paths of the last draw / last_draw_ms */
   uint64_t kernel_launches;        /* bounce launches timed (MRT_FLAG_PROFILE) */
-  double kernel_ms;                /* summed bounce-kernel time (MRT_FLAG_PROFILE) */
+  double kernel_ms;                /* summed bounce-kernel launch durations (MRT_FLAG_PROFILE) */
   uint64_t owned_pixels;
+  double kernel_busy_ms;           /* union of the bounce-kernel launch intervals: with frames in
+                                      flight launches overlap, so this is the kernel's busy time */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (gpurun_out/prof_<tag>_<cfg>) into profiles/.
+
+Writes:
+  profiles/<tag>_<cfg>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_<cfg>_summary.md         per-kernel timing + PMC-derived HBM traffic and SQ ratios
+  profiles/pmc_<cfg>.json                 HBM bytes per bounce launch (read by bench.py -> roofline.traffic)
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KB;
+on gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads,
+so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (FETCH and WRITE collected in
+separate passes).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path, kernel="bounce_kernel"):
+    agg, n = collections.defaultdict(float), collections.Counter()
+    meta = {}
+    for r in csv.DictReader(open(path)):
+        if kernel not in r["Kernel_Name"]:
+            continue
+        agg[r["Counter_Name"]] += float(r["Counter_Value"])
+        n[r["Counter_Name"]] += 1
+        meta = {k: r[k] for k in ("VGPR_Count", "SGPR_Count", "LDS_Block_Size", "Grid_Size", "Workgroup_Size")}
+    return {k: agg[k] / n[k] for k in agg}, meta
+
+
+def main(tag="r1", cfg="c2"):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{cfg}")
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    stats_csv = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copyfile(stats_csv, os.path.join(out, f"{tag}_{cfg}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats_csv)))
+    fetch, meta = counters(os.path.join(src, "fetch", "run_counter_collection.csv"))
+    write, _ = counters(os.path.join(src, "write", "run_counter_collection.csv"))
+    sq, _ = counters(os.path.join(src, "sq", "run_counter_collection.csv"))
+    clk, _ = counters(os.path.join(src, "clk", "run_counter_collection.csv"))
+    bounce = next(r for r in rows if "bounce_kernel" in r["Name"])
+    avg_ns = float(bounce["AverageNs"])
+    hbm = (2.0 * fetch["FETCH_SIZE"] + write["WRITE_SIZE"]) * 1024.0
+    lines = [f"# rocprofv3 summary — {tag} / {cfg}", "",
+             "`tools/profile.sh` → kernel trace + stats pass, then separate PMC passes "
+             "(FETCH_SIZE; WRITE_SIZE; SQ; GRBM), `bench.py --steps 2 --warmup 1`.", "",
+             "| kernel | calls | avg µs | total ms | % |", "|---|---|---|---|---|"]
+    for r in rows:
+        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.2f} |")
+    lines += ["", "## bounce_kernel PMC (per launch, averaged)", "",
+              f"* FETCH_SIZE {fetch['FETCH_SIZE']:.0f} KB (×2 gfx950 correction), WRITE_SIZE {write['WRITE_SIZE']:.0f} KB "
+              f"→ **HBM traffic {hbm / 1e6:.1f} MB per launch**, {hbm / (avg_ns * 1e-9) / 1e9:.0f} GB/s over the "
+              f"average launch ({avg_ns / 1e3:.1f} µs)",
+              f"* SQ: VALU insts {sq.get('SQ_INSTS_VALU', 0):.3g}, SALU {sq.get('SQ_INSTS_SALU', 0):.3g}, "
+              f"LDS {sq.get('SQ_INSTS_LDS', 0):.3g}, VMEM rd {sq.get('SQ_INSTS_VMEM_RD', 0):.3g}; "
+              f"WAIT_ANY / WAVE_CYCLES = {sq.get('SQ_WAIT_ANY', 0) / max(1, sq.get('SQ_WAVE_CYCLES', 1)):.2f}, "
+              f"ACTIVE_INST_VALU / WAVE_CYCLES = {sq.get('SQ_ACTIVE_INST_VALU', 0) / max(1, sq.get('SQ_WAVE_CYCLES', 1)):.2f}",
+              f"* effective clock ≈ GRBM_GUI_ACTIVE / 8 / launch = "
+              f"{clk.get('GRBM_GUI_ACTIVE', 0) / 8 / (avg_ns * 1e-9) / 1e9:.2f} GHz (reads high on overlapping dispatches)",
+              f"* dispatch: {meta}"]
+    with open(os.path.join(out, f"{tag}_{cfg}_summary.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    with open(os.path.join(out, f"pmc_{cfg}.json"), "w") as f:
+        json.dump({"tag": tag, "config": cfg, "kernel": "bounce_kernel", "hbm_bytes_per_launch": round(hbm),
+                   "fetch_size_kb": fetch["FETCH_SIZE"], "write_size_kb": write["WRITE_SIZE"],
+                   "avg_launch_ns_rocprof": avg_ns, "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024"},
+                  f, indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
