@@ -50,28 +50,39 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-frames", type=int, default=8, help="frames of the workload timed on the CPU oracle")
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="gloo = rehearsal of the N>1 path on fewer GPUs (reduce on a host copy)")
     return p.parse_args()
 
 
 def cpu_baseline(cfg, frames):
-    """The CPU oracle (scalar C++ restatement, oracle/) on a bounded sample:
-    the first `frames` frames of the same workload, std::thread over rows."""
+    """The CPU oracle (scalar C++ restatement, oracle/) on a bounded sample of
+    the same workload: `frames` frames over a row band sized so the sample is
+    ~10-30 s of CPU work, std::thread over rows (brute-force nearest hit)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
     import oracle  # test/baseline infrastructure only (see oracle/mrt_oracle.cpp header)
     import mrt
     if not os.path.exists(oracle.LIB_PATH):
         oracle.build()
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
     if cfg["procedural"]:
-        return None   # brute-force oracle on 1M triangles is not a bounded sample
+        return None   # brute force over 1M triangles is not a bounded sample
     sc = oracle.OracleScene(mrt.scene_path(cfg["scene"]), cfg["mtl"])
     W, H = cfg["width"], cfg["height"]
+    # brute force costs ~ triangles: keep ~16 M triangle-tests x bounces per thread-second budget
+    rows = H if sc.n_triangles <= 64 else max(8, min(H, int(H * 64 / sc.n_triangles * 8)))
+    mask = np.zeros((H, W), np.uint8)
+    y0 = (H - rows) // 2
+    mask[y0:y0 + rows] = 1
     t0 = time.perf_counter()
-    _, _ = sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads)
+    sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads, pixel_mask=mask)
     dt = time.perf_counter() - t0
-    return {"value": round(W * H * frames / dt / 1e6, 3), "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": f"frames 0-{frames - 1} of the workload ({W}x{H}, L={cfg['L']}, {W * H * frames} paths), "
-                      f"brute-force nearest hit, {threads} std::threads over rows, {dt:.2f} s wall"}
+    paths = W * rows * frames
+    return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": f"frames 0-{frames - 1}, rows {y0}-{y0 + rows - 1} of the workload ({W}x{rows} of {W}x{H}, "
+                      f"L={cfg['L']}, {paths} paths), brute-force nearest hit over {sc.n_triangles} triangles, "
+                      f"{threads} std::threads over rows, {dt:.2f} s wall"}
 
 
 def main():
@@ -85,13 +96,17 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    device = local_rank % max(1, torch.cuda.device_count())   # == local_rank on a full node
+    torch.cuda.set_device(device)
     torch.cuda.init()           # torch's HIP runtime first, then libmrt's (see mrt.py)
     import mrt
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
     W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
-    scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=local_rank)
+    scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=device)
     # the accumulation image lives in a torch tensor so RCCL can reduce it in
     # place; libmrt renders into it on its own stream (torch ships its own HIP
     # runtime copy, so streams are not shared: r.sync() orders the reduce)
@@ -106,7 +121,11 @@ def main():
         r.draw(spp)
         if world > 1:
             r.sync()
-            dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
+            if args.dist_backend == "nccl":
+                dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
+            else:
+                host = image.cpu()
+                dist.reduce(host, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -126,12 +145,13 @@ def main():
     elapsed = time.perf_counter() - t0
     st = r.stats()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tdev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([st["active_ray_bounces"] - base["active_ray_bounces"], st["paths"] - base["paths"],
-                            st["kernel_launches"] - base["kernel_launches"]], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([st["paths"] - base["paths"]], dtype=torch.float64, device=tdev)
         dist.all_reduce(tot)
+        assert int(tot.item()) == W * H * spp * args.steps, "ranks did not cover the frame"
     total_paths = W * H * spp * args.steps
     ms_per_step = elapsed / args.steps * 1e3
     value = total_paths / elapsed / 1e6

@@ -1217,7 +1217,10 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t* grid) {
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bounce_kernel<STACK, MODE>, kBlock, lds) != hipSuccess || n <= 0)
     n = 1;
-  *grid = (uint32_t)(prop.multiProcessorCount * std::min(n, 8));
+  // 4 blocks per CU per launch: with several frames in flight the launches of
+  // different frames share the CUs, and a smaller grid shortens the per-block
+  // segment scan (measured best on C2 at 1 and 8 shards)
+  *grid = (uint32_t)(prop.multiProcessorCount * std::min(n, 4));
   return hipSuccess;
 }
 
