@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 1
+#define MRT_ABI_VERSION 2
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -68,11 +68,13 @@ typedef struct mrt_scene_desc {
   uint32_t max_leaf_size;          /* BVH leaf size, 0 = default (4) */
   uint32_t lds_nodes;              /* top BVH nodes staged in LDS, 0 = default; UINT32_MAX = none */
   int device;                      /* HIP device ordinal; -1 = host only (import + BVH, no upload) */
+  uint32_t bvh_width;              /* 2 = BVH2, 4 = BVH4 (collapsed BVH2), 0 = default (4) */
 } mrt_scene_desc;
 
 typedef struct mrt_scene_info {
   uint32_t vertices, triangles, materials, light_triangles;
   uint32_t bvh_nodes, bvh_leaves, bvh_depth, bvh_lds_nodes;
+  uint32_t bvh_width, bvh_max_stack;   /* node width; traversal stack entries a ray can need */
   double bvh_sah_cost;
   double build_ms;                 /* host BVH build time */
   uint64_t device_bytes;           /* scene + BVH bytes resident on the device */

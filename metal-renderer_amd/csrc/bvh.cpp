@@ -5,6 +5,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <array>
 #include <deque>
 
 namespace mrt {
@@ -155,6 +156,7 @@ inline float bitsf(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indices, uint32_t num_triangles,
                const BvhBuildOptions& opt, BvhResult& out, std::string& error) {
   if (num_triangles == 0) { error = "empty scene"; return false; }
+  if (opt.width != 2 && opt.width != 4) { error = "BVH width must be 2 or 4"; return false; }
   if (opt.max_leaf_size == 0 || opt.max_leaf_size > (uint32_t)kMaxLeafSize) { error = "bad leaf size"; return false; }
   if (num_triangles >= (1u << (31 - kLeafCountBits))) { error = "too many triangles"; return false; }
   Builder b(opt);
@@ -174,20 +176,51 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
   b.build(0, num_triangles, 0);
   if (!b.err.empty()) { error = b.err; return false; }
 
-  // ---- layout: BFS for the top interior nodes, DFS below -----------------
+  // ---- collapse to the output width ----------------------------------------
+  // A wide node's children are found by repeatedly opening the largest-area
+  // interior child of the binary node (width 2 is the identity).
   const std::vector<BuildNode>& bn = b.nodes;
-  std::vector<int32_t> out_index(bn.size(), -1);
-  std::vector<int32_t> emit_order;   // build ids of interior nodes in output order
+  const uint32_t W = opt.width;
   auto is_leaf = [&](int32_t id) { return bn[id].child[0] < 0; };
+  auto collapse = [&](int32_t id, int32_t ch[4]) {
+    uint32_t n = 2;
+    ch[0] = bn[id].child[0];
+    ch[1] = bn[id].child[1];
+    while (n < W) {
+      int best = -1;
+      float best_area = -1.0f;
+      for (uint32_t i = 0; i < n; ++i)
+        if (!is_leaf(ch[i]) && bn[ch[i]].box.area() > best_area) { best = (int)i; best_area = bn[ch[i]].box.area(); }
+      if (best < 0) break;
+      const int32_t c = ch[best];
+      ch[best] = bn[c].child[0];
+      ch[n++] = bn[c].child[1];
+    }
+    return n;
+  };
+
+  // ---- layout: BFS for the top interior nodes, DFS below -----------------
+  std::vector<int32_t> out_index(bn.size(), -1);
+  std::vector<int32_t> emit_order;   // build ids of (wide) interior nodes in output order
+  std::vector<std::array<int32_t, 4>> wide_children;
+  std::vector<uint32_t> wide_count;
+  std::vector<uint32_t> stack_need;  // traversal stack entries pending when the node is entered
+  auto visit = [&](int32_t id) {
+    out_index[id] = (int32_t)emit_order.size();
+    emit_order.push_back(id);
+    std::array<int32_t, 4> ch{-1, -1, -1, -1};
+    wide_count.push_back(collapse(id, ch.data()));
+    wide_children.push_back(ch);
+  };
   if (!is_leaf(0)) {
     std::deque<int32_t> q{0};
     while (!q.empty() && emit_order.size() < opt.lds_node_budget) {
       const int32_t id = q.front();
       q.pop_front();
-      out_index[id] = (int32_t)emit_order.size();
-      emit_order.push_back(id);
-      for (int c = 0; c < 2; ++c)
-        if (!is_leaf(bn[id].child[c])) q.push_back(bn[id].child[c]);
+      visit(id);
+      const auto& ch = wide_children.back();
+      for (uint32_t c = 0; c < wide_count.back(); ++c)
+        if (!is_leaf(ch[c])) q.push_back(ch[c]);
     }
     out.lds_nodes = (uint32_t)emit_order.size();
     // remaining frontier subtrees in DFS order
@@ -197,12 +230,29 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
       while (!stack.empty()) {
         const int32_t id = stack.back();
         stack.pop_back();
-        out_index[id] = (int32_t)emit_order.size();
-        emit_order.push_back(id);
-        for (int c = 1; c >= 0; --c)
-          if (!is_leaf(bn[id].child[c])) stack.push_back(bn[id].child[c]);
+        visit(id);
+        const auto ch = wide_children.back();
+        for (int c = (int)wide_count.back() - 1; c >= 0; --c)
+          if (!is_leaf(ch[c])) stack.push_back(ch[c]);
       }
     }
+    // stack bound: entries pushed at the ancestors (all children but the one
+    // descended into) — parents are emitted before their children
+    stack_need.assign(emit_order.size(), 0);
+    uint32_t wide_depth_max = 0;
+    std::vector<uint32_t> wide_depth(emit_order.size(), 0);
+    for (size_t k = 0; k < emit_order.size(); ++k) {
+      const uint32_t below = stack_need[k] + (wide_count[k] - 1);
+      out.max_stack = std::max(out.max_stack, below);
+      wide_depth_max = std::max(wide_depth_max, wide_depth[k] + 1);
+      for (uint32_t c = 0; c < wide_count[k]; ++c) {
+        const int32_t cid = wide_children[k][c];
+        if (is_leaf(cid)) continue;
+        stack_need[out_index[cid]] = below;
+        wide_depth[out_index[cid]] = wide_depth[k] + 1;
+      }
+    }
+    out.wide_depth = wide_depth_max;
   }
   // leaf triangle runs in output order of their parents (DFS-ish locality)
   std::vector<int32_t> leaf_ref_of(bn.size(), 0);
@@ -228,13 +278,15 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
     emit_leaf(0);
     out.root = leaf_ref_of[0];
   } else {
-    for (int32_t id : emit_order)
-      for (int c = 0; c < 2; ++c)
-        if (is_leaf(bn[id].child[c])) emit_leaf(bn[id].child[c]);
+    for (size_t k = 0; k < emit_order.size(); ++k)
+      for (uint32_t c = 0; c < wide_count[k]; ++c)
+        if (is_leaf(wide_children[k][c])) emit_leaf(wide_children[k][c]);
     out.root = 0;
   }
+  out.width = W;
   out.num_nodes = (uint32_t)emit_order.size();
-  out.nodes.assign(16 * (size_t)std::max<uint32_t>(1, out.num_nodes), 0.0f);
+  const size_t node_floats = W == 4 ? 32 : 16;
+  out.nodes.assign(node_floats * (size_t)std::max<uint32_t>(1, out.num_nodes), 0.0f);
   auto padded = [](const Box& bx, float lo[3], float hi[3]) {
     for (int k = 0; k < 3; ++k) {
       const float m = std::max(std::fabs(bx.lo[k]), std::fabs(bx.hi[k]));
@@ -243,27 +295,42 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
       hi[k] = bx.hi[k] + pad;
     }
   };
+  auto child_ref = [&](int32_t cid) { return is_leaf(cid) ? leaf_ref_of[cid] : out_index[cid]; };
   double sah = 0.0;
   const double root_area = std::max(1e-30, (double)bn[0].box.area());
   for (size_t k = 0; k < emit_order.size(); ++k) {
     const BuildNode& n = bn[emit_order[k]];
-    float* o = &out.nodes[16 * k];
-    float l_lo[3], l_hi[3], r_lo[3], r_hi[3];
-    const BuildNode& L = bn[n.child[0]];
-    const BuildNode& R = bn[n.child[1]];
-    padded(L.box, l_lo, l_hi);
-    padded(R.box, r_lo, r_hi);
-    o[0] = l_lo[0]; o[1] = l_hi[0]; o[2] = l_lo[1]; o[3] = l_hi[1];
-    o[4] = r_lo[0]; o[5] = r_hi[0]; o[6] = r_lo[1]; o[7] = r_hi[1];
-    o[8] = l_lo[2]; o[9] = l_hi[2]; o[10] = r_lo[2]; o[11] = r_hi[2];
-    const int32_t lref = is_leaf(n.child[0]) ? leaf_ref_of[n.child[0]] : out_index[n.child[0]];
-    const int32_t rref = is_leaf(n.child[1]) ? leaf_ref_of[n.child[1]] : out_index[n.child[1]];
-    o[12] = bitsf((uint32_t)lref);
-    o[13] = bitsf((uint32_t)rref);
+    float* o = &out.nodes[node_floats * k];
     sah += opt.traversal_cost * n.box.area() / root_area;
-    if (is_leaf(n.child[0])) sah += (double)L.count * L.box.area() / root_area;
-    if (is_leaf(n.child[1])) sah += (double)R.count * R.box.area() / root_area;
+    for (uint32_t c = 0; c < wide_count[k]; ++c) {
+      const BuildNode& C = bn[wide_children[k][c]];
+      if (is_leaf(wide_children[k][c])) sah += (double)C.count * C.box.area() / root_area;
+    }
+    if (W == 2) {
+      float l_lo[3], l_hi[3], r_lo[3], r_hi[3];
+      padded(bn[wide_children[k][0]].box, l_lo, l_hi);
+      padded(bn[wide_children[k][1]].box, r_lo, r_hi);
+      o[0] = l_lo[0]; o[1] = l_hi[0]; o[2] = l_lo[1]; o[3] = l_hi[1];
+      o[4] = r_lo[0]; o[5] = r_hi[0]; o[6] = r_lo[1]; o[7] = r_hi[1];
+      o[8] = l_lo[2]; o[9] = l_hi[2]; o[10] = r_lo[2]; o[11] = r_hi[2];
+      o[12] = bitsf((uint32_t)child_ref(wide_children[k][0]));
+      o[13] = bitsf((uint32_t)child_ref(wide_children[k][1]));
+    } else {
+      // BVH4: component-major (SoA within the node), see mrt_layout.h
+      for (uint32_t c = 0; c < 4; ++c) {
+        if (c < wide_count[k]) {
+          float lo[3], hi[3];
+          padded(bn[wide_children[k][c]].box, lo, hi);
+          for (int a = 0; a < 3; ++a) { o[8 * a + c] = lo[a]; o[8 * a + 4 + c] = hi[a]; }
+          o[24 + c] = bitsf((uint32_t)child_ref(wide_children[k][c]));
+        } else {
+          for (int a = 0; a < 3; ++a) { o[8 * a + c] = 0.0f; o[8 * a + 4 + c] = 0.0f; }
+          o[24 + c] = bitsf((uint32_t)kEmptyChild);
+        }
+      }
+    }
   }
+  if (is_leaf(0)) out.wide_depth = 0;
   (void)fbits;
   out.sah_cost = sah;
   out.max_depth = b.max_depth;

@@ -26,16 +26,20 @@ struct BvhBuildOptions {
   uint32_t lds_node_budget = 256; // interior nodes placed first in BFS order
   uint32_t bins = 16;
   float traversal_cost = 1.0f;    // relative to one triangle test
+  uint32_t width = 2;             // 2 = BVH2 (64-B nodes), 4 = BVH4 (128-B nodes, collapsed BVH2)
 };
 
 struct BvhResult {
-  std::vector<float> nodes;       // 16 floats per interior node
+  std::vector<float> nodes;       // 16 (BVH2) or 32 (BVH4) floats per interior node
   std::vector<float> tris;        // 12 floats per leaf-ordered triangle
   int32_t root = 0;
   uint32_t num_nodes = 0;
   uint32_t num_leaves = 0;
   uint32_t max_depth = 0;         // deepest leaf (root = 0); traversal needs <= max_depth stack entries
   uint32_t lds_nodes = 0;         // top BFS-ordered nodes (min(budget, num_nodes))
+  uint32_t width = 2;
+  uint32_t max_stack = 0;         // traversal stack entries needed (push all hit children but one)
+  uint32_t wide_depth = 0;        // interior levels of the emitted tree
   double sah_cost = 0.0;
 };
 

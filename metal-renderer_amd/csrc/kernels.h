@@ -47,6 +47,8 @@ struct BounceArgs {
   const float4* noise_shade;   // slot (f+i)%3
   float4* radiance;            // per-frame path radiance, written once per owned pixel when
                                // its path ends (accumulated afterwards by launch_accumulate_frame)
+  uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
+                               // [max_stack - stack_entries][grid * 256] uint32 (null if none)
 };
 
 // running-mean accumulation of one frame over the owned tiles
@@ -73,7 +75,8 @@ struct AccumArgs {
                                float* image, hipStream_t s);                                              \
   /* persistent grid size of the fused bounce kernel for this scene */                                    \
   hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                 \
-  /* fused wavefront bounce over `grid` blocks (the same grid for every launch of a renderer) */          \
+  /* fused wavefront bounce over `grid` blocks (the same grid for every launch of a renderer);          \
+     stack_entries = LDS stack capacity 8/16/24/32, deeper entries go to a.stack_spill */                 \
   hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
                            uint32_t grid, hipStream_t s);                                                 \
   /* accumulateImage over the owned tiles of one frame (in frame order) */                                 \

@@ -9,6 +9,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -33,12 +34,6 @@ constexpr int kBlock = 256;   // 4 waves of 64 lanes
 #define MRT_SHADE_BARRIER() __builtin_amdgcn_sched_barrier(0)
 #else
 #define MRT_SHADE_BARRIER() do {} while (0)
-#endif
-#ifndef MRT_WAVE_TRAVERSAL
-#define MRT_WAVE_TRAVERSAL 0   // measured slower than per-lane traversal on C2 (4140 vs 4820 Mpaths/s)
-#endif
-#ifndef MRT_WHILE_WHILE
-#define MRT_WHILE_WHILE 1      // +3-4 % over the if-if loop on C2
 #endif
 // Minimum waves per SIMD for the bounce kernel (launch bounds): 6 caps it at
 // 80 VGPRs with a few scratch spills and measured +16 % over the 94-VGPR,
@@ -182,6 +177,31 @@ __device__ __forceinline__ void box2(const float4& a, const float4& b, const flo
   hr = tnr <= tfr;
 }
 
+// Box test of the four children of a BVH4 node (component-major node, see
+// mrt_layout.h); returns each child's entry distance, +inf for a miss or an
+// empty slot.
+__device__ __forceinline__ void box4(const float4* q, V3 o, const RayBox& rb, float tmin, float tmax, float tn[4]) {
+#if MRT_PRECISE
+  const float ox = o.x, oy = o.y, oz = o.z;
+  const float oix = 0.0f, oiy = 0.0f, oiz = 0.0f;
+#else
+  const float ox = 0.0f, oy = 0.0f, oz = 0.0f;
+  const float oix = rb.oinv.x, oiy = rb.oinv.y, oiz = rb.oinv.z;
+  (void)o;
+#endif
+  const float* f = reinterpret_cast<const float*>(q);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float x0 = slab(f[k], ox, rb.inv.x, oix), x1 = slab(f[4 + k], ox, rb.inv.x, oix);
+    const float y0 = slab(f[8 + k], oy, rb.inv.y, oiy), y1 = slab(f[12 + k], oy, rb.inv.y, oiy);
+    const float z0 = slab(f[16 + k], oz, rb.inv.z, oiz), z1 = slab(f[20 + k], oz, rb.inv.z, oiz);
+    const float tnear = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));
+    const float tfar = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
+    const bool live = (int32_t)fbits(f[24 + k]) != kEmptyChild;
+    tn[k] = (live & (tnear <= tfar)) ? tnear : __builtin_inff();
+  }
+}
+
 // LDS staging modes:
 //   kGlobal  — only the per-lane traversal stack lives in LDS (stage ABI kernels);
 //   kTopLds  — the first n BFS-ordered BVH nodes (top levels) are staged in
@@ -206,16 +226,31 @@ struct LdsCtx {
   uint32_t light_base;
   uint32_t scratch_base;  // uint32 offset of the per-block scratch
   uint32_t stack_base;    // uint32 offset of this lane's stack slot 0
+  uint32_t* spill;        // stack entries >= STACK: this lane's column of a global
+  uint32_t spill_stride;  //   [entry][lane] spill area (null when STACK covers the BVH)
 };
 
 __device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
 
 // float4 counts of the staged scene image for a mode
-__host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t nodes, uint32_t lds_nodes, uint32_t tris,
-                                                      uint32_t mats, uint32_t lights) {
-  if (mode == kAllLds) return 4 * nodes + 3 * tris + 6 * tris + 2 * mats + 7 * lights;
-  if (mode == kTopLds) return 4 * lds_nodes;
+// (node_f4 = float4s per node: 4 for BVH2, 8 for BVH4)
+__host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t node_f4, uint32_t nodes, uint32_t lds_nodes,
+                                                      uint32_t tris, uint32_t mats, uint32_t lights) {
+  if (mode == kAllLds) return node_f4 * nodes + 3 * tris + 6 * tris + 2 * mats + 7 * lights;
+  if (mode == kTopLds) return node_f4 * lds_nodes;
   return 0;
+}
+
+template <int MODE>
+__device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx& cx, int32_t node, float4* q) {
+  if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) q[i] = g_lds[8 * node + i];
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 8 * (size_t)node;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) q[i] = p[i];
+  }
 }
 
 template <int MODE>
@@ -266,36 +301,47 @@ __device__ __forceinline__ float4 fetch_light(const DeviceScene& sc, const LdsCt
   return reinterpret_cast<const float4*>(sc.lights)[7 * l + i];
 }
 
+// STACK = LDS entries per lane; a negative STACK means |STACK| LDS entries
+// plus the global spill area for deeper entries.
+template <int STACK>
 __device__ __forceinline__ void stack_push(const LdsCtx& cx, int sp, int32_t v) {
-  lds_u32()[cx.stack_base + sp * kBlock] = (uint32_t)v;
+  constexpr int kL = STACK < 0 ? -STACK : STACK;
+  if (STACK > 0 || sp < kL) lds_u32()[cx.stack_base + sp * kBlock] = (uint32_t)v;
+  else cx.spill[(size_t)(sp - kL) * cx.spill_stride] = (uint32_t)v;
 }
+template <int STACK>
 __device__ __forceinline__ int32_t stack_get(const LdsCtx& cx, int sp) {
-  return (int32_t)lds_u32()[cx.stack_base + sp * kBlock];
+  constexpr int kL = STACK < 0 ? -STACK : STACK;
+  if (STACK > 0 || sp < kL) return (int32_t)lds_u32()[cx.stack_base + sp * kBlock];
+  return (int32_t)cx.spill[(size_t)(sp - kL) * cx.spill_stride];
 }
 
 // Stage the LDS image for `MODE` (every thread of the block calls it);
 // `scratch_u32` uint32 words of per-block scratch follow the scene image.
 template <int MODE>
-__device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scratch_u32) {
+__device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scratch_u32, uint32_t* spill = nullptr) {
   LdsCtx cx;
+  const uint32_t nf4 = 2 * sc.width;   // float4s per node
   const uint32_t n_nodes = (MODE == kAllLds) ? sc.num_nodes : (MODE == kTopLds ? sc.lds_nodes : 0u);
   const uint32_t T = (MODE == kAllLds) ? sc.num_triangles : 0u;
   const uint32_t M = (MODE == kAllLds) ? sc.num_materials : 0u;
   const uint32_t NL = (MODE == kAllLds) ? sc.num_lights + 1 : 0u;
   cx.n_lds_nodes = n_nodes;
-  cx.tri_base = 4 * n_nodes;
+  cx.tri_base = nf4 * n_nodes;
   cx.prim_base = cx.tri_base + 3 * T;
   cx.mat_base = cx.prim_base + 6 * T;
   cx.light_base = cx.mat_base + 2 * M;
   const uint32_t f4 = cx.light_base + 7 * NL;
   cx.scratch_base = 4 * f4;
   cx.stack_base = cx.scratch_base + ((scratch_u32 + 3) & ~3u) + threadIdx.x;
+  cx.spill_stride = gridDim.x * kBlock;
+  cx.spill = spill ? spill + blockIdx.x * kBlock + threadIdx.x : nullptr;
   if (MODE != kGlobal) {
     const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes), reinterpret_cast<const float4*>(sc.tris),
                             reinterpret_cast<const float4*>(sc.prims), reinterpret_cast<const float4*>(sc.materials),
                             reinterpret_cast<const float4*>(sc.lights)};
     const uint32_t base[5] = {0u, cx.tri_base, cx.prim_base, cx.mat_base, cx.light_base};
-    const uint32_t len[5] = {4 * n_nodes, 3 * T, 6 * T, 2 * M, 7 * NL};
+    const uint32_t len[5] = {nf4 * n_nodes, 3 * T, 6 * T, 2 * M, 7 * NL};
     for (int r = 0; r < 5; ++r)
       for (uint32_t i = threadIdx.x; i < len[r]; i += kBlock) g_lds[base[r] + i] = src[r][i];
     __syncthreads();
@@ -307,65 +353,71 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
 // 64-lane waves): a lane that reaches a leaf parks it and keeps descending
 // interior nodes until every lane of the wave holds a leaf, then the wave
 // tests leaves together — interior and leaf work are not interleaved lane by
-// lane.  The per-lane stack is in LDS; DONE marks an empty stack.
+// lane.  The per-lane stack is in LDS (entries beyond STACK spill to global
+// memory); kDone marks an empty stack.
 // ANY = false: nearest hit in [tmin, h.t]; ties -> lowest primitive index.
 // ANY = true:  stop at the first primitive k != target with (t_k, k) <
 //              (t_target, target) in [0, t_target] (shadow occlusion).
-
-#if !MRT_WHILE_WHILE
-// "if-if" loop: one node or one leaf per iteration.
-template <int STACK, int MODE, bool ANY>
-__device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
-                                         uint32_t target) {
-  const RayBox rb = make_raybox(o, d);
-  int32_t node = sc.root;
-  int sp = 0;
-  while (true) {
-    if (node >= 0) {
-      float4 a, b, c, e;
-      fetch_node<MODE>(sc, cx, node, a, b, c, e);
-      bool hl, hr;
-      float tnl, tnr;
-      box2(a, b, c, o, rb, tmin, h.t, hl, hr, tnl, tnr);
-      const int32_t rl = (int32_t)fbits(e.x), rr = (int32_t)fbits(e.y);
-      if (hl && hr) {
-        const bool swap = tnr < tnl;
-        const int32_t nearer = swap ? rr : rl, farther = swap ? rl : rr;
-        if (sp < STACK) { stack_push(cx, sp, farther); ++sp; }
-        node = nearer;
-        continue;
-      }
-      if (hl) { node = rl; continue; }
-      if (hr) { node = rr; continue; }
-    } else {
-      const uint32_t lr = ~(uint32_t)node;
-      const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
-      for (uint32_t k = 0; k < cnt; ++k) {
-        float4 t0, t1, t2;
-        fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
-        const uint32_t prim = fbits(t0.w);
-        float t, u, v;
-        const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v);
-        if (ANY) {
-          if (hit & (prim != target) & ((t < h.t) | (prim < target))) return true;
-        } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
-          h.found = true;
-          h.t = t;
-          h.u = u;
-          h.v = v;
-          h.prim = prim;
-        }
-      }
-    }
-    if (sp == 0) break;
-    --sp;
-    node = stack_get(cx, sp);
-  }
-  return false;
-}
-#else
+// Both results are independent of the visiting order, so the BVH2 and BVH4
+// walks return the same (brute-force) answer.
 constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
-template <int STACK, int MODE, bool ANY>
+
+template <int STACK>
+__device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
+  const int32_t n = sp > 0 ? stack_get<STACK>(cx, sp - 1) : kDone;
+  sp = max(sp - 1, 0);
+  return n;
+}
+
+// One interior node: returns the next node to visit (nearest hit child, or a
+// popped entry, or kDone); the other hit children are pushed far-to-near.
+template <int STACK, int MODE, int WIDTH>
+__device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const LdsCtx& cx, int32_t node, V3 o,
+                                                 const RayBox& rb, float tmin, float tmax, int& sp) {
+  if constexpr (WIDTH == 2) {
+    float4 a, b, c, e;
+    fetch_node<MODE>(sc, cx, node, a, b, c, e);
+    bool hl, hr;
+    float tnl, tnr;
+    box2(a, b, c, o, rb, tmin, tmax, hl, hr, tnl, tnr);
+    const int32_t rl = (int32_t)fbits(e.x), rr = (int32_t)fbits(e.y);
+    if (!(hl | hr)) return stack_pop<STACK>(cx, sp);
+    const bool right_first = !hl || (hr && tnr < tnl);
+    if (hl & hr) {
+      stack_push<STACK>(cx, sp, right_first ? rl : rr);
+      ++sp;
+    }
+    return right_first ? rr : rl;
+  } else {
+    float4 q[7];
+    fetch_node4<MODE>(sc, cx, node, q);
+    float t[4];
+    box4(q, o, rb, tmin, tmax, t);
+    int32_t r[4] = {(int32_t)fbits(q[6].x), (int32_t)fbits(q[6].y), (int32_t)fbits(q[6].z), (int32_t)fbits(q[6].w)};
+    // 4-input sorting network on (t, ref); misses (+inf) sink to the end
+#define MRT_CE(i, j)                                      \
+    {                                                     \
+      const bool sw_ = t[j] < t[i];                       \
+      const float ti_ = sw_ ? t[j] : t[i];                \
+      const int32_t ri_ = sw_ ? r[j] : r[i];              \
+      t[j] = sw_ ? t[i] : t[j];                           \
+      r[j] = sw_ ? r[i] : r[j];                           \
+      t[i] = ti_;                                         \
+      r[i] = ri_;                                         \
+    }
+    MRT_CE(0, 1) MRT_CE(2, 3) MRT_CE(0, 2) MRT_CE(1, 3) MRT_CE(1, 2)
+#undef MRT_CE
+    const float inf = __builtin_inff();
+    if (t[3] < inf) { stack_push<STACK>(cx, sp, r[3]); ++sp; }
+    if (t[2] < inf) { stack_push<STACK>(cx, sp, r[2]); ++sp; }
+    if (t[1] < inf) { stack_push<STACK>(cx, sp, r[1]); ++sp; }
+    int32_t next = r[0];
+    if (!(t[0] < inf)) next = stack_pop<STACK>(cx, sp);
+    return next;
+  }
+}
+
+template <int STACK, int MODE, int WIDTH, bool ANY>
 __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
                                          uint32_t target) {
   const RayBox rb = make_raybox(o, d);
@@ -375,27 +427,10 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
   while (node != kDone || leaf != 0) {
     // interior nodes
     while (node != kDone && node >= 0) {
-      float4 a, b, c, e;
-      fetch_node<MODE>(sc, cx, node, a, b, c, e);
-      bool hl, hr;
-      float tnl, tnr;
-      box2(a, b, c, o, rb, tmin, h.t, hl, hr, tnl, tnr);
-      const int32_t rl = (int32_t)fbits(e.x), rr = (int32_t)fbits(e.y);
-      if (hl | hr) {
-        const bool right_first = !hl || (hr && tnr < tnl);
-        node = right_first ? rr : rl;
-        if (hl & hr) {
-          if (sp < STACK) stack_push(cx, sp, right_first ? rl : rr);
-          sp = min(sp + 1, STACK);
-        }
-      } else {
-        node = sp > 0 ? stack_get(cx, sp - 1) : kDone;
-        sp = max(sp - 1, 0);
-      }
+      node = interior_step<STACK, MODE, WIDTH>(sc, cx, node, o, rb, tmin, h.t, sp);
       if (node < 0 && leaf == 0) {   // park the leaf, keep descending
         leaf = node;
-        node = sp > 0 ? stack_get(cx, sp - 1) : kDone;
-        sp = max(sp - 1, 0);
+        node = stack_pop<STACK>(cx, sp);
       }
       if (!__any(leaf == 0)) break;
     }
@@ -422,17 +457,14 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
       leaf = 0;
       if (node < 0) {   // the next node is a leaf too: take it now
         leaf = node;
-        node = sp > 0 ? stack_get(cx, sp - 1) : kDone;
-        sp = max(sp - 1, 0);
+        node = stack_pop<STACK>(cx, sp);
       }
     }
   }
   return false;
 }
 
-#endif
-
-template <int STACK, int MODE>
+template <int STACK, int MODE, int WIDTH>
 __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
                                              float tmax) {
   Hit h;
@@ -440,137 +472,30 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
-  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u);
+  traverse<STACK, MODE, WIDTH, false>(sc, cx, o, d, tmin, h, 0u);
   return h;
 }
 
-template <int STACK, int MODE>
+template <int STACK, int MODE, int WIDTH>
 __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
                                                float t_target) {
   Hit h;
   h.t = t_target;
   h.found = false;
-  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target);
-}
-
-// Wave-coherent ("packet") traversal for small scenes (kAllLds).  The whole
-// 64-lane wave walks the BVH together: node and triangle addresses are
-// wave-uniform (LDS broadcast reads, no bank conflicts, uniform branches), the
-// wave descends into a child when ANY live lane's box test passes, and one
-// wave-uniform stack (the lane-0 column of the per-lane stack) holds deferred
-// children.  Every lane tests a superset of the triangles its own traversal
-// would reach, with the same acceptance rule, so each lane's nearest hit is
-// exactly the per-lane (and brute-force) result.  Must be called by every
-// lane of the wave; `enabled` masks lanes without a ray.
-template <int STACK, int MODE, bool ANY>
-__device__ __forceinline__ bool traverse_wave(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
-                                              uint32_t target, bool enabled) {
-  const RayBox rb = make_raybox(o, d);
-  const uint32_t wstack = cx.stack_base - (threadIdx.x & 63u);   // lane-0 column of this wave
-  bool live = enabled;
-  bool occluded = false;
-  if (!__any(live)) return false;
-  int32_t node = sc.root;
-  int sp = 0;
-  while (true) {
-    if (node >= 0) {
-      float4 a, b, c, e;
-      fetch_node<MODE>(sc, cx, node, a, b, c, e);
-      bool hl, hr;
-      float tnl, tnr;
-      box2(a, b, c, o, rb, tmin, h.t, hl, hr, tnl, tnr);
-      hl = hl & live;
-      hr = hr & live;
-      const uint64_t ml = __ballot(hl), mr = __ballot(hr);
-      const int32_t rl = __builtin_amdgcn_readfirstlane((int32_t)fbits(e.x));
-      const int32_t rr = __builtin_amdgcn_readfirstlane((int32_t)fbits(e.y));
-      if (ml | mr) {
-        // majority vote on the nearer child among the lanes that hit one
-        const uint64_t pl = __ballot(hl & (!hr | (tnl <= tnr)));
-        const bool left_first = ml && (!mr || 2 * __popcll(pl) >= __popcll(ml | mr));
-        if (ml && mr) {
-          if (sp < STACK) lds_u32()[wstack + sp * kBlock] = (uint32_t)(left_first ? rr : rl);
-          sp = min(sp + 1, STACK);
-        }
-        node = left_first ? rl : rr;
-        continue;
-      }
-    } else {
-      const uint32_t lr = ~(uint32_t)node;
-      const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
-      for (uint32_t k = 0; k < cnt; ++k) {
-        float4 t0, t1, t2;
-        fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
-        const uint32_t prim = __builtin_amdgcn_readfirstlane(fbits(t0.w));
-        if (live) {
-          float t, u, v;
-          if (tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v)) {
-            if (ANY) {
-              if (prim != target && (t < h.t || prim < target)) {
-                occluded = true;
-                live = false;
-              }
-            } else if (!h.found || t < h.t || prim < h.prim) {
-              h.found = true;
-              h.t = t;
-              h.u = u;
-              h.v = v;
-              h.prim = prim;
-            }
-          }
-        }
-      }
-      if (ANY && !__any(live)) break;
-    }
-    if (sp == 0) break;
-    --sp;
-    node = __builtin_amdgcn_readfirstlane((int32_t)lds_u32()[wstack + sp * kBlock]);
-  }
-  return occluded;
-}
-
-template <int STACK, int MODE>
-__device__ __forceinline__ Hit trace_nearest_wave(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
-                                                  float tmax, bool enabled) {
-  Hit h;
-  h.t = tmax;
-  h.u = h.v = 0.0f;
-  h.prim = 0xFFFFFFFFu;
-  h.found = false;
-  traverse_wave<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u, enabled);
-  return h;
-}
-
-// Shadow visibility, wave-coherent form of shadow_reaches_target (below).
-template <int STACK, int MODE>
-__device__ __forceinline__ bool shadow_reaches_target_wave(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d,
-                                                           uint32_t target, bool enabled) {
-  float tT = 0.0f;
-  bool ok = false;
-  if (enabled) {
-    const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
-    const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
-    float u, v;
-    ok = tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) && (tT >= kDistanceEpsilon);
-  }
-  Hit h;
-  h.t = tT;
-  h.found = false;
-  const bool occ = traverse_wave<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, ok);
-  return ok && !occ;
+  return traverse<STACK, MODE, WIDTH, true>(sc, cx, o, d, 0.0f, h, target);
 }
 
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
 // (renderer/Shaders.metal:214-231): contributes iff the nearest hit of the
 // shadow ray (tmin 0, tmax inf) is the target triangle at t >= 1e-4.
-template <int STACK, int MODE>
+template <int STACK, int MODE, int WIDTH>
 __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target) {
   const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
   float tT, u, v;
   if (!tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v)) return false;
   if (!(tT >= kDistanceEpsilon)) return false;
-  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT);
+  return !trace_occluded<STACK, MODE, WIDTH>(sc, cx, o, d, target, tT);
 }
 
 // ---------------------------------------------------------------------------
@@ -932,14 +857,14 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n
   return total;
 }
 
-template <int STACK, int MODE>
+template <int STACK, int MODE, int WIDTH>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
   __shared__ uint32_t s_cursor;
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
-  const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1);
+  const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1, a.stack_spill);
   uint32_t* seg = lds_u32() + cx.scratch_base;   // exclusive prefix of the input segments
   if (tid == 0) s_cursor = 0;
 
@@ -1011,8 +936,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     // -- phase 1: nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
     Hit h;
     h.found = false;
-    if (MRT_WAVE_TRAVERSAL && MODE == kAllLds) h = trace_nearest_wave<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff(), active);
-    else if (active) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+    if (active) h = trace_nearest<STACK, MODE, WIDTH>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
     STAMP(1);
     // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
     //    near hit ends the path (:122-126)
@@ -1039,10 +963,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     }
     STAMP(2);
     // -- phase 3: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
-    if (MRT_WAVE_TRAVERSAL && MODE == kAllLds) {
-      const bool vis = (a.debug & 1u) ? sh.valid : shadow_reaches_target_wave<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target, sh.valid);
-      if (vis) s.R = add(s.R, sh.L);
-    } else if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target))) {
+    if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE, WIDTH>(sc, cx, sh.o, sh.d, sh.target))) {
       s.R = add(s.R, sh.L);
     }
     STAMP(3);
@@ -1108,6 +1029,7 @@ __global__ __launch_bounds__(kBlock) void raygen_kernel(uint32_t W, uint32_t H, 
   for (int k = 0; k < 3; ++k) { r.throughput[k] = 1.0f; r.radiance[k] = 0.0f; }
 }
 
+template <int WIDTH>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DeviceScene sc, const uint8_t* rays, uint32_t stride,
                                                            uint32_t count, RefIntersection* out) {
   const LdsCtx cx = stage_lds<kGlobal>(sc, 0);
@@ -1117,7 +1039,8 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DeviceScene sc, const
   RefIntersection res{-1.0f, 0xFFFFFFFFu, {0.0f, 0.0f}};
   const float tmax = r[7];
   if (tmax >= 0.0f) {   // maxDistance < 0 disables the ray (Shaders.metal:124,173)
-    const Hit h = trace_nearest<kMaxStack, kGlobal>(sc, cx, mk(r[0], r[1], r[2]), mk(r[4], r[5], r[6]), r[3], tmax);
+    const V3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
+    const Hit h = trace_nearest<kMaxStack, kGlobal, WIDTH>(sc, cx, o, d, r[3], tmax);
     if (h.found) {
       res.distance = h.t;
       res.triangleIndex = h.prim;
@@ -1191,20 +1114,40 @@ inline uint32_t blocks_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 constexpr size_t kAllLdsBudget = 48 * 1024;   // scene bytes staged whole in LDS
 
 int choose_mode(const DeviceScene& sc) {
-  if ((size_t)lds_scene_float4s(kAllLds, sc.num_nodes, 0, sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16 <=
-      kAllLdsBudget)
+  static const int forced = [] {   // MRT_MODE=0/1/2 forces kGlobal/kTopLds/kAllLds (profiling)
+    const char* v = std::getenv("MRT_MODE");
+    return v ? std::atoi(v) : -1;
+  }();
+  if (forced >= 0 && forced <= 2) return forced;
+  if ((size_t)lds_scene_float4s(kAllLds, 2 * sc.width, sc.num_nodes, 0, sc.num_triangles, sc.num_materials,
+                                sc.num_lights + 1) * 16 <= kAllLdsBudget)
     return kAllLds;
   return sc.lds_nodes > 0 ? kTopLds : kGlobal;
 }
 
 size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
-  const size_t scene = (size_t)lds_scene_float4s(mode, sc.num_nodes, sc.lds_nodes, sc.num_triangles,
+  const size_t scene = (size_t)lds_scene_float4s(mode, 2 * sc.width, sc.num_nodes, sc.lds_nodes, sc.num_triangles,
                                                  sc.num_materials, sc.num_lights + 1) * 16;
   const size_t scratch = ((size_t)grid + 1 + 3) / 4 * 16;
-  return scene + scratch + (size_t)stack * kBlock * 4;
+  return scene + scratch + (size_t)stack * kBlock * 4;   // stack = LDS entries (|STACK|)
 }
 
-template <int STACK, int MODE>
+// kTopLds: stage only as many top BVH nodes as keep the block's LDS within
+// 1/6 of the CU (the VGPR budget allows 6 resident blocks of 4 waves); the
+// BFS order makes any prefix the top levels.  Fewer staged nodes and full
+// occupancy beat more staged nodes (C4: 64 nodes 737 vs 128 nodes 715 Mpaths/s).
+constexpr size_t kLdsPerBlockTarget = 160 * 1024 / 6;
+DeviceScene fit_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
+  if (mode != kTopLds) return sc;
+  DeviceScene f = sc;
+  const size_t fixed = bounce_lds_bytes(sc, kGlobal, stack, grid) + 64;   // scratch + stack + static
+  const size_t node_bytes = (size_t)sc.width * 32;
+  const size_t fit = fixed < kLdsPerBlockTarget ? (kLdsPerBlockTarget - fixed) / node_bytes : 0;
+  f.lds_nodes = (uint32_t)std::min<size_t>(sc.lds_nodes, fit);
+  return f;
+}
+
+template <int STACK, int MODE, int WIDTH>
 hipError_t grid_for(const DeviceScene& sc, uint32_t* grid) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -1213,40 +1156,62 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t* grid) {
   e = hipGetDeviceProperties(&prop, dev);
   if (e != hipSuccess) return e;
   // the scratch depends on the grid: size with the worst case (8 blocks/CU)
-  const size_t lds = bounce_lds_bytes(sc, MODE, STACK, (uint32_t)prop.multiProcessorCount * 8);
+  const uint32_t worst_grid = (uint32_t)prop.multiProcessorCount * 8;
+  const DeviceScene f = fit_lds_nodes(sc, MODE, STACK < 0 ? -STACK : STACK, worst_grid);
+  const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, worst_grid);
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bounce_kernel<STACK, MODE>, kBlock, lds) != hipSuccess || n <= 0)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bounce_kernel<STACK, MODE, WIDTH>, kBlock, lds) != hipSuccess || n <= 0)
     n = 1;
-  // 4 blocks per CU per launch: with several frames in flight the launches of
-  // different frames share the CUs, and a smaller grid shortens the per-block
-  // segment scan (measured best on C2 at 1 and 8 shards)
-  *grid = (uint32_t)(prop.multiProcessorCount * std::min(n, 4));
+  // LDS-resident scenes: 4 blocks per CU per launch — with several frames in
+  // flight the launches of different frames share the CUs, and a smaller grid
+  // shortens the per-block segment scan (measured best on C2 at 1 and 8
+  // shards).  Scenes traversed from global memory are latency-bound: 6 blocks
+  // per CU (C4 +6 %, C3 +2 % over 4).
+  *grid = (uint32_t)(prop.multiProcessorCount * std::min(n, MODE == kAllLds ? 4 : 6));
   return hipSuccess;
 }
 
-template <int STACK, int MODE>
+template <int STACK, int MODE, int WIDTH>
 hipError_t launch_bounce_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
-  const size_t lds = bounce_lds_bytes(sc, MODE, STACK, grid);
-  bounce_kernel<STACK, MODE><<<dim3(grid), dim3(kBlock), lds, s>>>(sc, a);
+  const DeviceScene f = fit_lds_nodes(sc, MODE, STACK < 0 ? -STACK : STACK, grid);
+  const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, grid);
+  bounce_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
   return hipGetLastError();
 }
 
-template <int STACK>
+template <int STACK, int WIDTH>
 hipError_t dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
                          hipStream_t s) {
   switch (choose_mode(sc)) {
-    case kAllLds: return a ? launch_bounce_t<STACK, kAllLds>(sc, *a, grid, s) : grid_for<STACK, kAllLds>(sc, grid_out);
-    case kTopLds: return a ? launch_bounce_t<STACK, kTopLds>(sc, *a, grid, s) : grid_for<STACK, kTopLds>(sc, grid_out);
-    default: return a ? launch_bounce_t<STACK, kGlobal>(sc, *a, grid, s) : grid_for<STACK, kGlobal>(sc, grid_out);
+    case kAllLds:
+      return a ? launch_bounce_t<STACK, kAllLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kAllLds, WIDTH>(sc, grid_out);
+    case kTopLds:
+      return a ? launch_bounce_t<STACK, kTopLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kTopLds, WIDTH>(sc, grid_out);
+    default:
+      return a ? launch_bounce_t<STACK, kGlobal, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kGlobal, WIDTH>(sc, grid_out);
   }
 }
 
+template <int STACK>
+hipError_t dispatch_width(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
+                          hipStream_t s) {
+  return sc.width == 4 ? dispatch_mode<STACK, 4>(sc, a, grid, grid_out, s)
+                       : dispatch_mode<STACK, 2>(sc, a, grid, grid_out, s);
+}
+
+// stack_entries = LDS stack capacity (8/16/24/32); when the BVH's bound is
+// larger, the spill variants (8, 16 or 32 LDS entries + global) are used
 hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_entries, uint32_t grid,
                     uint32_t* grid_out, hipStream_t s) {
-  if (stack_entries <= 8) return dispatch_mode<8>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 16) return dispatch_mode<16>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 24) return dispatch_mode<24>(sc, a, grid, grid_out, s);
-  return dispatch_mode<32>(sc, a, grid, grid_out, s);
+  if (sc.max_stack > stack_entries) {
+    if (stack_entries <= 8) return dispatch_width<-8>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 16) return dispatch_width<-16>(sc, a, grid, grid_out, s);
+    return dispatch_width<-32>(sc, a, grid, grid_out, s);
+  }
+  if (stack_entries <= 8) return dispatch_width<8>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 16) return dispatch_width<16>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 24) return dispatch_width<24>(sc, a, grid, grid_out, s);
+  return dispatch_width<32>(sc, a, grid, grid_out, s);
 }
 
 }  // namespace
@@ -1260,8 +1225,13 @@ hipError_t launch_raygen(uint32_t W, uint32_t H, const float* noise, RefRay* ray
 hipError_t launch_intersect(const DeviceScene& sc, const void* rays, uint32_t stride, uint32_t count,
                             RefIntersection* out, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  intersect_kernel<<<dim3(blocks_for(count)), dim3(kBlock), (size_t)kMaxStack * kBlock * 4, s>>>(sc,
-                     reinterpret_cast<const uint8_t*>(rays), stride, count, out);
+  const size_t lds = (size_t)kMaxStack * kBlock * 4;
+  if (sc.width == 4)
+    intersect_kernel<4><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, reinterpret_cast<const uint8_t*>(rays),
+                                                                           stride, count, out);
+  else
+    intersect_kernel<2><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, reinterpret_cast<const uint8_t*>(rays),
+                                                                           stride, count, out);
   return hipGetLastError();
 }
 

@@ -9,7 +9,8 @@
 //        * ray queue: SoA of four float4 planes (16-B lane loads, 1 KiB per
 //          wave instruction, fully coalesced);
 //        * BVH2 nodes: 64-B records (both child boxes + child refs) so one
-//          node visit is four 16-B loads from one 64-B line;
+//          node visit is four 16-B loads from one 64-B line; BVH4 nodes:
+//          128-B component-major records (four child boxes + refs);
 //        * leaf triangles: {v0|prim, e1, e2} float4 triples in leaf order;
 //        * per-primitive shading records (positions, normals, material and
 //          light ids) in primitive order so a hit gathers 6 x 16 B with no
@@ -65,16 +66,24 @@ static_assert(sizeof(RefLightTriangle) == 100, "RefLightTriangle");
 //   [2] = (L.lo.z, L.hi.z, R.lo.z, R.hi.z)
 //   [3] = (bits(Lref), bits(Rref), 0, 0)
 // ref >= 0: interior node index; ref < 0: leaf, ~ref = (first << 4) | (count-1)
+//
+// BVH4 node i = nodes[8i .. 8i+7] (128 B, two 64-B lines), component-major so
+// one 16-B load yields one box component for all four children:
+//   [0] = lo.x[0..3]  [1] = hi.x[0..3]  [2] = lo.y[0..3]  [3] = hi.y[0..3]
+//   [4] = lo.z[0..3]  [5] = hi.z[0..3]  [6] = bits(ref[0..3])  [7] = 0
+// Unused child slots carry ref == kEmptyChild (and a zero box); the traversal
+// masks them by ref, never by box.
+constexpr int32_t kEmptyChild = 0x7FFFFFFF;
 constexpr int kLeafCountBits = 4;
 constexpr int kMaxLeafSize = 1 << kLeafCountBits;   // 16
-constexpr int kMaxStack = 32;                       // traversal stack entries per ray (LDS)
-constexpr int kMaxBvhDepth = kMaxStack;             // builder forces leaves below this depth
+constexpr int kMaxBvhDepth = 32;                    // builder forces leaves below this binary depth
+constexpr int kMaxStack = 48;                       // traversal stack entries per ray (BVH4 bound < 1.5 x depth)
 
 // Device-resident scene, passed to kernels by value.  Every pointer is
 // 16-B aligned device memory; float pointers documented as "float4" hold
 // 4 floats per record.
 struct DeviceScene {
-  const float* nodes;        // float4 x 4 per BVH node (see above)
+  const float* nodes;        // float4 x 4 (BVH2) or x 8 (BVH4) per node (see above)
   const float* tris;         // float4 x 3 per leaf-ordered triangle: (v0, bits(prim)), (e1, 0), (e2, 0)
   const float* prims;        // float4 x 6 per primitive (original order):
                              //   (p0, bits(material)), (p1, bits(light index or ~0u)), (p2, 0),
@@ -89,6 +98,8 @@ struct DeviceScene {
   uint32_t num_materials;
   uint32_t num_lights;       // light triangles, excluding the sentinel (SharedData.lightTrianglesCount)
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
+  uint32_t width;            // 2 = BVH2, 4 = BVH4
+  uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxStack)
 };
 
 }  // namespace mrt

@@ -86,6 +86,7 @@ struct FrameSlot {
   DevBuf queue[2][4];
   DevBuf segments;          // 2 x grid per-block survivor counts + 2 chunk words
   DevBuf radiance;          // W*H float4, written once per owned pixel per frame
+  DevBuf spill;             // traversal stack entries beyond the LDS capacity (deep BVHs)
   hipEvent_t acc_done = nullptr;
 };
 
@@ -212,6 +213,9 @@ int alloc_frame_buffers(mrt_renderer* r) {
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(slots * 16));
     HIP_TRY(fs.radiance.alloc((size_t)W * H * 16));
+    const uint32_t need = r->scene->dev.max_stack;
+    if (need > r->stack_entries && !fs.spill.p)
+      HIP_TRY(fs.spill.alloc((size_t)(need - r->stack_entries) * r->grid * 256 * 4));
   }
   if (r->own_image) {
     if (r->image) (void)hipFree(r->image);
@@ -376,15 +380,19 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (desc->max_leaf_size) opt.max_leaf_size = desc->max_leaf_size;
   if (desc->lds_nodes == UINT32_MAX) opt.lds_node_budget = 0;
   else if (desc->lds_nodes) opt.lds_node_budget = desc->lds_nodes;
-  else opt.lds_node_budget = 128;
+  else opt.lds_node_budget = 256;   // BFS prefix; the launcher stages what fits (fit_lds_nodes)
+  if (const char* v = std::getenv("MRT_LDS_NODES"); v && !desc->lds_nodes) opt.lds_node_budget = (uint32_t)std::strtoul(v, nullptr, 0);
   // tuning overrides (profiling): MRT_LEAF = max leaf size, MRT_CTRAV = SAH node cost
   if (const char* v = std::getenv("MRT_LEAF")) opt.max_leaf_size = (uint32_t)std::strtoul(v, nullptr, 0);
   if (const char* v = std::getenv("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
+  opt.width = desc->bvh_width ? desc->bvh_width : 4;
+  if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (opt.width != 2 && opt.width != 4) return fail(MRT_ERR_INVALID, "bvh_width must be 2 or 4");
   const auto t0 = std::chrono::steady_clock::now();
   if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), h.indices.data(), T, opt, s->bvh, err))
     return fail(MRT_ERR_INVALID, "BVH build failed: " + err);
   const double build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (s->bvh.max_depth >= (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_INVALID, "BVH deeper than the traversal stack");
+  if (s->bvh.max_stack > (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack");
 
   // per-primitive shading records (primitive order)
   std::vector<float> prims((size_t)T * 24);
@@ -428,6 +436,8 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   in.bvh_leaves = s->bvh.num_leaves;
   in.bvh_depth = s->bvh.max_depth;
   in.bvh_lds_nodes = s->bvh.lds_nodes;
+  in.bvh_width = s->bvh.width;
+  in.bvh_max_stack = s->bvh.max_stack;
   in.bvh_sah_cost = s->bvh.sah_cost;
   in.build_ms = build_ms;
   if (desc->device < 0) {   // host-only scene (CPU tests of import + BVH)
@@ -452,6 +462,8 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.num_materials = (uint32_t)h.materials.size();
   d.num_lights = h.light_count;
   d.lds_nodes = s->bvh.lds_nodes;
+  d.width = s->bvh.width;
+  d.max_stack = s->bvh.max_stack;
   in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
   *out = s.release();
   return MRT_OK;
@@ -483,9 +495,10 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
   std::vector<uint8_t> seen(T, 0);
   auto fbits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
   // returns false on violation; checks triangle containment in the given box
-  struct Item { int32_t ref; float lo[3], hi[3]; uint32_t depth; };
+  // pend = stack entries pushed by the ancestors (bounded by b.max_stack)
+  struct Item { int32_t ref; float lo[3], hi[3]; uint32_t depth, pend; };
   std::vector<Item> stack;
-  Item root{b.root, {-1e30f, -1e30f, -1e30f}, {1e30f, 1e30f, 1e30f}, 0};
+  Item root{b.root, {-1e30f, -1e30f, -1e30f}, {1e30f, 1e30f, 1e30f}, 0, 0};
   stack.push_back(root);
   uint32_t nodes_seen = 0;
   while (!stack.empty()) {
@@ -495,13 +508,29 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
     if (it.ref >= 0) {
       if ((uint32_t)it.ref >= b.num_nodes) return fail(MRT_ERR_STATE, "BVH node index out of range");
       ++nodes_seen;
-      const float* n = &b.nodes[16 * (size_t)it.ref];
-      Item l{(int32_t)fbits(n[12]), {n[0], n[2], n[8]}, {n[1], n[3], n[9]}, it.depth + 1};
-      Item r{(int32_t)fbits(n[13]), {n[4], n[6], n[10]}, {n[5], n[7], n[11]}, it.depth + 1};
-      for (int k = 0; k < 3; ++k)
-        if (!(l.lo[k] <= l.hi[k]) || !(r.lo[k] <= r.hi[k])) return fail(MRT_ERR_STATE, "BVH empty child box");
-      stack.push_back(l);
-      stack.push_back(r);
+      Item ch[4];
+      uint32_t nc = 0;
+      if (b.width == 2) {
+        const float* n = &b.nodes[16 * (size_t)it.ref];
+        ch[nc++] = Item{(int32_t)fbits(n[12]), {n[0], n[2], n[8]}, {n[1], n[3], n[9]}, it.depth + 1, 0};
+        ch[nc++] = Item{(int32_t)fbits(n[13]), {n[4], n[6], n[10]}, {n[5], n[7], n[11]}, it.depth + 1, 0};
+      } else {
+        const float* n = &b.nodes[32 * (size_t)it.ref];
+        for (int c = 0; c < 4; ++c) {
+          const int32_t ref = (int32_t)fbits(n[24 + c]);
+          if (ref == mrt::kEmptyChild) continue;
+          if (nc != (uint32_t)c) return fail(MRT_ERR_STATE, "BVH4 empty slot before a used one");
+          ch[nc++] = Item{ref, {n[c], n[8 + c], n[16 + c]}, {n[4 + c], n[12 + c], n[20 + c]}, it.depth + 1, 0};
+        }
+        if (nc < 2) return fail(MRT_ERR_STATE, "BVH4 node with fewer than two children");
+      }
+      for (uint32_t c = 0; c < nc; ++c) {
+        for (int k = 0; k < 3; ++k)
+          if (!(ch[c].lo[k] <= ch[c].hi[k])) return fail(MRT_ERR_STATE, "BVH empty child box");
+        ch[c].pend = it.pend + nc - 1;
+        if (ch[c].pend > b.max_stack) return fail(MRT_ERR_STATE, "BVH stack bound too small");
+        stack.push_back(ch[c]);
+      }
     } else {
       const uint32_t leaf = ~(uint32_t)it.ref;
       const uint32_t first = leaf >> mrt::kLeafCountBits, cnt = (leaf & (mrt::kMaxLeafSize - 1)) + 1;
@@ -610,8 +639,17 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   r->image = desc->image;
   HIP_TRY(hipEventCreate(&r->ev_start));
   HIP_TRY(hipEventCreate(&r->ev_stop));
-  const uint32_t depth = desc->scene->bvh.max_depth;
-  r->stack_entries = depth <= 8 ? 8 : depth <= 16 ? 16 : depth <= 24 ? 24 : 32;
+  // LDS stack capacity: the BVH's bound rounded up to 8/16 entries when it is
+  // <= 16; deeper BVHs keep 8 entries in LDS and spill the rest to global
+  // memory (MRT_STACK overrides the cap).  LDS per block bounds the resident
+  // blocks per CU, and for global-memory traversal occupancy wins: C4 with
+  // 8 LDS entries + spill ran 1.5x faster than with a 32-entry LDS stack.
+  const uint32_t need = desc->scene->bvh.max_stack;
+  uint32_t cap = need <= 16 ? 16 : 8;
+  if (const char* v = std::getenv("MRT_STACK")) cap = std::max<uint32_t>(8, (uint32_t)std::strtoul(v, nullptr, 0));
+  const uint32_t want = std::min(need, cap);
+  r->stack_entries = want <= 8 ? 8 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
+  if (need > r->stack_entries) r->stack_entries = r->stack_entries <= 8 ? 8 : r->stack_entries <= 16 ? 16 : 32;   // spill variants
   if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
   if (const char* v = std::getenv("MRT_INFLIGHT")) r->inflight = (uint32_t)std::strtoul(v, nullptr, 0);
   r->inflight = std::max<uint32_t>(1, std::min<uint32_t>(3, r->inflight));
@@ -717,6 +755,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.noise_raygen = reinterpret_cast<const float4*>(noise_ptr(r, (int64_t)f));
       a.noise_shade = reinterpret_cast<const float4*>(noise_ptr(r, mrt::noise_frame_for_iteration((int64_t)f, b)));
       a.radiance = fs.radiance.as<float4>();
+      a.stack_spill = fs.spill.as<uint32_t>();
       if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
       HIP_TRY(launch_bounce(r, a, fs.stream));
       if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));

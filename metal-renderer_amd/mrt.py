@@ -53,6 +53,7 @@ class SceneDesc(ctypes.Structure):
         ("max_leaf_size", ctypes.c_uint32),
         ("lds_nodes", ctypes.c_uint32),
         ("device", ctypes.c_int),
+        ("bvh_width", ctypes.c_uint32),
     ]
 
 
@@ -60,7 +61,8 @@ class SceneInfo(ctypes.Structure):
     _fields_ = [
         ("vertices", ctypes.c_uint32), ("triangles", ctypes.c_uint32), ("materials", ctypes.c_uint32),
         ("light_triangles", ctypes.c_uint32), ("bvh_nodes", ctypes.c_uint32), ("bvh_leaves", ctypes.c_uint32),
-        ("bvh_depth", ctypes.c_uint32), ("bvh_lds_nodes", ctypes.c_uint32), ("bvh_sah_cost", ctypes.c_double),
+        ("bvh_depth", ctypes.c_uint32), ("bvh_lds_nodes", ctypes.c_uint32), ("bvh_width", ctypes.c_uint32),
+        ("bvh_max_stack", ctypes.c_uint32), ("bvh_sah_cost", ctypes.c_double),
         ("build_ms", ctypes.c_double), ("device_bytes", ctypes.c_uint64),
     ]
 
@@ -170,10 +172,11 @@ class Scene:
     """Flattened scene + BVH on the device (initRaytracing, Renderer.mm:255-470)."""
 
     def __init__(self, obj: str, mtl_override: str | None = None, *, procedural_triangles: int = 0,
-                 procedural_seed: int = 1, max_leaf_size: int = 0, lds_nodes: int = 0, device: int = 0):
+                 procedural_seed: int = 1, max_leaf_size: int = 0, lds_nodes: int = 0, device: int = 0,
+                 bvh_width: int = 0):
         self._h = None
         d = SceneDesc(scene_path(obj).encode(), (mtl_override or "").encode(), procedural_triangles,
-                      procedural_seed, max_leaf_size, lds_nodes, device)
+                      procedural_seed, max_leaf_size, lds_nodes, device, bvh_width)
         h = ctypes.c_void_p()
         _check(lib().mrt_scene_create(ctypes.byref(d), ctypes.byref(h)), "mrt_scene_create")
         self._h = h

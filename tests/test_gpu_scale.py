@@ -17,11 +17,12 @@ from helpers import SEED, compare_to_golden, dev_ptr, from_dev, pixel_metrics, t
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def proc_scenes(gpu, mrt_mod, oracle_mod):
+@pytest.fixture(scope="module", params=[2, 4], ids=["bvh2", "bvh4"])
+def proc_scenes(request, gpu, mrt_mod, oracle_mod):
     """cornellbox + an 8192-triangle procedural sphere, product and oracle
     built from the same flattened buffers."""
-    sc = mrt_mod.Scene("cornellbox", procedural_triangles=8192, procedural_seed=11, lds_nodes=64)
+    sc = mrt_mod.Scene("cornellbox", procedural_triangles=8192, procedural_seed=11, lds_nodes=64,
+                       bvh_width=request.param)
     e = sc.export()
     osc = oracle_mod.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
     assert sc.info["bvh_nodes"] > sc.info["bvh_lds_nodes"] > 0   # top levels in LDS, the rest global
@@ -46,8 +47,12 @@ def test_deep_bvh_intersect_bitexact(proc_scenes, mrt_mod, oracle_mod):
     assert (ref["distance"] > 0).mean() > 0.5
 
 
-def test_deep_bvh_render_parity(proc_scenes, mrt_mod):
+@pytest.mark.parametrize("lds_stack", ["32", "8"], ids=["lds", "spill"])
+def test_deep_bvh_render_parity(proc_scenes, mrt_mod, monkeypatch, lds_stack):
+    """Whole renders on the deep BVH; "lds" holds the whole traversal stack in
+    LDS, "spill" keeps 8 entries in LDS and the deeper ones in global memory."""
     sc, osc = proc_scenes
+    monkeypatch.setenv("MRT_STACK", lds_stack)
     W, H, L, frames = 64, 48, 4, 2
     ref, A = osc.render(W, H, L, SEED, frames, threads=8)
     r = mrt_mod.Renderer(sc, W, H, L, precise=True)

@@ -24,6 +24,7 @@ static float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static V cross(V a, V b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 static uint32_t fb(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 
+static bool g_cull = true;
 struct Counts { int steps = 0, inner = 0, leaves = 0, tris = 0; float t = INFINITY; };
 
 static Counts trace(const BvhResult& b, V o, V d) {
@@ -31,9 +32,35 @@ static Counts trace(const BvhResult& b, V o, V d) {
   V inv = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
   int32_t node = b.root;
   std::vector<int32_t> st;
+  std::vector<float> st_t;
   while (true) {
     c.steps++;
-    if (node >= 0) {
+    if (node >= 0 && b.width == 4) {
+      // BVH4: test 4 children, descend into the nearest hit, push the others
+      // far-to-near with their entry distance (culled on pop)
+      c.inner++;
+      const float* n = &b.nodes[32 * (size_t)node];
+      float tn[4];
+      int32_t ref[4];
+      int hits = 0;
+      for (int k = 0; k < 4; ++k) {
+        ref[k] = (int32_t)fb(n[24 + k]);
+        float a0 = (n[k] - o.x) * inv.x, a1 = (n[4 + k] - o.x) * inv.x;
+        float b0 = (n[8 + k] - o.y) * inv.y, b1 = (n[12 + k] - o.y) * inv.y;
+        float c0 = (n[16 + k] - o.z) * inv.z, c1 = (n[20 + k] - o.z) * inv.z;
+        float t0 = std::max(std::max(std::min(a0, a1), std::min(b0, b1)), std::max(std::min(c0, c1), 0.0f));
+        float t1 = std::min(std::min(std::max(a0, a1), std::max(b0, b1)), std::min(std::max(c0, c1), c.t));
+        tn[k] = (ref[k] != 0x7FFFFFFF && t0 <= t1) ? t0 : INFINITY;
+        hits += tn[k] < INFINITY;
+      }
+      if (hits) {
+        int idx[4] = {0, 1, 2, 3};
+        std::sort(idx, idx + 4, [&](int a, int bb) { return tn[a] < tn[bb]; });
+        for (int k = hits - 1; k >= 1; --k) { st.push_back(ref[idx[k]]); st_t.push_back(tn[idx[k]]); }
+        node = ref[idx[0]];
+        continue;
+      }
+    } else if (node >= 0) {
       c.inner++;
       const float* n = &b.nodes[16 * (size_t)node];
       auto box = [&](float x0, float x1, float y0, float y1, float z0, float z1, float& tn) {
@@ -71,6 +98,18 @@ static Counts trace(const BvhResult& b, V o, V d) {
         if (tt >= 0 && tt <= c.t) c.t = tt;
       }
     }
+    if (b.width == 4) {
+      bool found = false;
+      while (!st.empty()) {
+        node = st.back();
+        float t = st_t.back();
+        st.pop_back();
+        st_t.pop_back();
+        if (t <= c.t || !g_cull) { found = true; break; }
+      }
+      if (!found) break;
+      continue;
+    }
     if (st.empty()) break;
     node = st.back();
     st.pop_back();
@@ -82,6 +121,8 @@ int main(int argc, char** argv) {
   const std::string obj = argc > 1 ? argv[1] : "../tests/golden/scenes/cornellbox.obj";
   const uint32_t proc = argc > 2 ? (uint32_t)atoi(argv[2]) : 0;
   const uint32_t leaf = argc > 3 ? (uint32_t)atoi(argv[3]) : 4;
+  const uint32_t width = argc > 4 ? (uint32_t)atoi(argv[4]) : 2;
+  g_cull = argc > 5 ? atoi(argv[5]) != 0 : true;
   HostScene sc;
   std::string err;
   if (!import_obj(obj, "", sc, err)) { std::fprintf(stderr, "%s\n", err.c_str()); return 1; }
@@ -89,11 +130,13 @@ int main(int argc, char** argv) {
   flatten(sc);
   BvhBuildOptions opt;
   opt.max_leaf_size = leaf;
+  opt.width = width;
   BvhResult b;
   if (!build_bvh(sc.vertices.data()->v, sizeof(RefVertex), sc.indices.data(), (uint32_t)sc.references.size(), opt, b,
                  err)) { std::fprintf(stderr, "%s\n", err.c_str()); return 1; }
-  std::printf("%s: %zu tris, %u nodes, %u leaves, depth %u, SAH %.2f\n", obj.c_str(), sc.references.size(),
-              b.num_nodes, b.num_leaves, b.max_depth, b.sah_cost);
+  std::printf("%s: %zu tris, BVH%u %u nodes, %u leaves, depth %u (wide %u), stack %u, SAH %.2f\n", obj.c_str(),
+              sc.references.size(), b.width, b.num_nodes, b.num_leaves, b.max_depth, b.wide_depth, b.max_stack,
+              b.sah_cost);
   const uint32_t W = 256, H = 144;
   std::mt19937 rng(5);
   std::uniform_real_distribution<float> U(0.0f, 1.0f);
