@@ -9,8 +9,10 @@ accumulation image to rank 0.  value = paths of all ranks / max-over-ranks
 step time (strong scaling: the frame is split into 64x64 tiles, tile t on
 rank t % N).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
 For N > 1 launch with torch.distributed.run (one process per GPU).
+--shard-of S (N = 1 only): render only rank 0's tiles of an S-way split —
+one GPU's share of a multi-GPU job, value = that share's paths/s (diagnostic).
 """
 from __future__ import annotations
 
@@ -37,6 +39,10 @@ CONFIGS = {
     # configs[3]: 1M-triangle procedural mesh in the cornellbox shell, 64 spp, L = 4
     "c4": dict(workload="C4 1M-triangle procedural mesh 1920x1080 64spp L=4", scene="cornellbox", mtl=None,
                width=1920, height=1080, spp=64, L=4, procedural=1 << 20),
+    # configs[4]: C4's scene at 4K, 256 spp, L = 8 — the 8-GPU configuration
+    # (one GPU's share is measured with --shard-of 8)
+    "c5": dict(workload="C5 1M-triangle procedural mesh 3840x2160 256spp L=8", scene="cornellbox", mtl=None,
+               width=3840, height=2160, spp=256, L=8, procedural=1 << 20),
 }
 
 
@@ -50,6 +56,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-frames", type=int, default=8, help="frames of the workload timed on the CPU oracle")
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
+    p.add_argument("--shard-of", type=int, default=0,
+                   help="N=1 only: time rank 0's tiles of an S-way tile split (one GPU's share)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="gloo = rehearsal of the N>1 path on fewer GPUs (reduce on a host copy)")
     return p.parse_args()
@@ -93,6 +101,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    shard_count = world
+    if args.shard_of:
+        if world > 1:
+            raise SystemExit("--shard-of is a single-process diagnostic")
+        shard_count = args.shard_of
     import torch
     import torch.distributed as dist
 
@@ -112,7 +125,7 @@ def main():
     # runtime copy, so streams are not shared: r.sync() orders the reduce)
     image = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
-    r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True, shard_rank=rank, shard_count=world,
+    r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True, shard_rank=rank, shard_count=shard_count,
                      image_ptr=image.data_ptr())
     r.prepare(spp)
 
@@ -153,25 +166,28 @@ def main():
         dist.all_reduce(tot)
         assert int(tot.item()) == W * H * spp * args.steps, "ranks did not cover the frame"
     total_paths = W * H * spp * args.steps
+    if args.shard_of:
+        total_paths = st["paths"] - base["paths"]   # this GPU's share only
     ms_per_step = elapsed / args.steps * 1e3
     value = total_paths / elapsed / 1e6
 
     # roofline of the dominant kernel (the fused bounce kernel: every launch of
-    # the frame is one) from HIP events recorded around each launch on the
-    # stream it runs on, over the timed steps of this rank.  With frames in
-    # flight the launches overlap, so two rates are reported:
-    #   achieved       = algorithmic bytes per launch / average launch duration
-    #                    (the definition rocprofv3's per-dispatch average checks)
-    #   achieved_busy  = algorithmic bytes / union of the launch intervals
+    # the frame is one) from HIP events recorded around the launches of every
+    # 8th frame on the stream they run on, over the timed steps of this rank
+    # (timing events serialise a stream, so timing every launch would cost
+    # 3-20 %).  With frames in flight the launches overlap, so two rates:
+    #   achieved      = algorithmic bytes per launch / average launch duration
+    #                   (the definition rocprofv3's per-dispatch average checks)
+    #   achieved_job  = algorithmic bytes of the timed steps / their wall time
     A = st["active_ray_bounces"] - base["active_ray_bounces"]
     P = st["paths"] - base["paths"]
     launches = st["kernel_launches"] - base["kernel_launches"]
+    timed = st["timed_launches"] - base["timed_launches"]
     kms = st["kernel_ms"] - base["kernel_ms"]
-    busy_ms = st["kernel_busy_ms"] - base["kernel_busy_ms"]
     bytes_alg = B_PATH * P + B_BOUNCE * A
-    avg_launch_ms = kms / max(1, launches)
-    achieved = (bytes_alg / max(1, launches)) / (avg_launch_ms * 1e-3) / 1e9 if launches else 0.0
-    achieved_busy = bytes_alg / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+    avg_launch_ms = kms / max(1, timed)
+    achieved = (bytes_alg / max(1, launches)) / (avg_launch_ms * 1e-3) / 1e9 if timed else 0.0
+    achieved_job = bytes_alg / elapsed / 1e9
     traffic = None
     pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
     if os.path.exists(pmc_path):
@@ -194,18 +210,19 @@ def main():
                 (f" + seeded procedural mesh ({cfg['procedural']} tris)" if cfg["procedural"] else "") +
                 ", deterministic noise seed",
         "config": {"workload": cfg["workload"], "width": W, "height": H, "spp": spp, "max_path_length": L,
-                   "scene": cfg["scene"], "parallelism": f"tiles64x{world}" + (" + rccl reduce" if world > 1 else ""),
+                   "scene": cfg["scene"], "parallelism": (f"tile shard 0 of {shard_count} (one GPU's share)" if args.shard_of else
+                                   f"tiles64x{world}" + (" + rccl reduce" if world > 1 else "")),
                    "build": "precise" if args.precise else "fast"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "achieved_busy": round(achieved_busy, 1), "frac_busy": round(achieved_busy / HBM_PEAK_GBS, 4),
-                     "busy_ms_per_step": round(busy_ms / max(1, args.steps), 3),
-                     "kernel": "bounce_kernel", "launches": launches, "avg_launch_ms": round(avg_launch_ms, 4),
+                     "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),
+                     "kernel": "bounce_kernel", "launches": launches, "timed_launches": timed,
+                     "avg_launch_ms": round(avg_launch_ms, 4),
                      "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
                      "active_ray_bounces_per_step": int(A / max(1, args.steps))},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames)
     if rank == 0:
         print(json.dumps(result), flush=True)

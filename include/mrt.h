@@ -54,7 +54,8 @@ typedef enum mrt_status {
 
 /* flags */
 #define MRT_FLAG_PRECISE 1u   /* parity kernels: IEEE div/sqrt, no FMA contraction, CR sin/cos */
-#define MRT_FLAG_PROFILE 2u   /* time every bounce launch with HIP events (mrt_stats.kernel_ms) */
+#define MRT_FLAG_PROFILE 2u   /* time the bounce launches of every 8th frame with HIP events (mrt_stats.kernel_ms);
+                                 timing events serialise a stream's launches, so only a sample is timed */
 
 typedef struct mrt_scene mrt_scene;
 typedef struct mrt_renderer mrt_renderer;
@@ -133,11 +134,10 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
   uint64_t active_ray_bounces;     /* A: rays alive at the start of each bounce, summed */
   double last_draw_ms;             /* GPU time of the last draw/draw_n (HIP events) */
   double mpaths_per_s;             /* paths of the last draw / last_draw_ms */
-  uint64_t kernel_launches;        /* bounce launches timed (MRT_FLAG_PROFILE) */
-  double kernel_ms;                /* summed bounce-kernel launch durations (MRT_FLAG_PROFILE) */
+  uint64_t kernel_launches;        /* bounce-kernel launches issued */
+  double kernel_ms;                /* summed durations of the timed launches (MRT_FLAG_PROFILE) */
   uint64_t owned_pixels;
-  double kernel_busy_ms;           /* union of the bounce-kernel launch intervals: with frames in
-                                      flight launches overlap, so this is the kernel's busy time */
+  uint64_t timed_launches;         /* launches behind kernel_ms (every 8th frame's) */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);

@@ -14,7 +14,9 @@
 namespace mrt {
 
 // Ray queue: SoA of four float4 planes, one record per ray slot:
-//   plane 0: (origin.xyz, bits(pixel | prevDiffuse << 31))   = Ray.origin, params.y
+//   plane 0: (origin.xyz, bits(slot | prevDiffuse << 31))    = Ray.origin, params.y
+//            slot = frame_in_batch * num_slots + owned slot (the pixel's
+//            radiance index; the pixel is decoded from it, kernels.hip)
 //   plane 1: (direction.xyz, 0)                            = Ray.direction
 //   plane 2: (throughput.rgb, material pdf)                = Ray.throughput, params.x
 //   plane 3: (radiance.rgb, ior)                           = Ray.radiance, params.w
@@ -25,13 +27,19 @@ struct RayQueue {
   float4* plane[4];
 };
 
+// Frame batching: one launch carries the rays of `batch` consecutive frames
+// (frame_index .. frame_index + batch - 1), so a GPU that owns a small share
+// of the tiles still issues launches of full-frame size.
+constexpr uint32_t kMaxBatch = 8;
+
 struct BounceArgs {
   uint32_t width, height;
-  uint32_t frame_index;        // SharedData.frameIndex
+  uint32_t frame_index;        // SharedData.frameIndex of the batch's first frame
+  uint32_t batch;              // frames in this launch (1..kMaxBatch)
   uint32_t bounce;             // loop iteration i (renderer/Renderer.mm:517)
   uint32_t max_path_length;    // MAX_PATH_LENGTH
   uint32_t shard_rank, shard_count, tiles_x;
-  uint32_t num_slots;          // bounce 0 input: owned tiles * 4096 pixel slots
+  uint32_t num_slots;          // per frame: owned tiles * 4096 pixel slots (bounce 0 input = num_slots * batch)
   uint32_t debug;              // ablation bits for profiling (0 in production, env MRT_DEBUG):
                                //   1 = skip shadow traversal, 2 = skip shading, 4 = no queue writes
   // segmented queues: block g of a launch appends its survivors to slots
@@ -43,10 +51,13 @@ struct BounceArgs {
   uint32_t* out_chunk;
   uint32_t* out_total;         // survivors of this launch (stats)
   RayQueue in_q, out_q;
-  const float4* noise_raygen;  // slot f%3  = T_f
-  const float4* noise_shade;   // slot (f+i)%3
-  float4* radiance;            // per-frame path radiance, written once per owned pixel when
-                               // its path ends (accumulated afterwards by launch_accumulate_frame)
+  // noise: the table of frame g (T_g, or the initial table for g < 0) is
+  // noise_window[(noise_offset + g - frame_index) * 4096 ...]; raygen reads
+  // T_f, iteration i reads T_{f - c(i)} (noise.h); noise_offset >= 2
+  const float4* noise_window;
+  uint32_t noise_offset;
+  float4* radiance;            // [batch][num_slots] path radiance by owned slot, written once per
+                               // owned pixel when its path ends (accumulated by launch_accumulate_frame)
   uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
                                // [max_stack - stack_entries][grid * 256] uint32 (null if none)
 };
@@ -54,10 +65,11 @@ struct BounceArgs {
 // running-mean accumulation of one frame over the owned tiles
 struct AccumArgs {
   uint32_t width, height;
-  uint32_t frame_index;
+  uint32_t frame_index;        // first frame of the batch; frames are applied in order
+  uint32_t batch;
   uint32_t shard_rank, shard_count, tiles_x;
   uint32_t num_slots;          // owned tiles * 4096
-  const float4* radiance;
+  const float4* radiance;      // [batch][num_slots]
   float4* image;
 };
 
@@ -79,7 +91,7 @@ struct AccumArgs {
      stack_entries = LDS stack capacity 8/16/24/32, deeper entries go to a.stack_spill */                 \
   hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
                            uint32_t grid, hipStream_t s);                                                 \
-  /* accumulateImage over the owned tiles of one frame (in frame order) */                                 \
+  /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \
   hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s);                                  \
   /* diagnostic phase stamps (MRT_STAMPS builds; zeros otherwise) */                                      \
   hipError_t read_stamps(unsigned long long* out8, bool reset);                                          \

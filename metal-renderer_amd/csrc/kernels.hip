@@ -669,6 +669,25 @@ __device__ __forceinline__ void camera_ray(uint32_t x, uint32_t y, uint32_t W, u
   o = mk(0.0f, 1.0f, 2.35f);   // up - view * 2.35
 }
 
+// Owned slots: slot s of a frame = owned tile k = s >> 12 (global tile
+// rank + k * count) and pixel p = s & 4095 inside it in 8x8-block order (a
+// wave's 64 lanes cover one 8x8 block).  A ray's tag is its global slot
+// g = frame_in_batch * num_slots + s — at bounce 0 simply the launch index.
+__device__ __forceinline__ void slot_pixel(uint32_t s, uint32_t rank, uint32_t count, uint32_t tiles_x, uint32_t& x,
+                                           uint32_t& y) {
+  const uint32_t k = s >> 12, p = s & 4095u;
+  const uint32_t t = rank + k * count;
+  const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+  const uint32_t blk = p >> 6, q = p & 63u;
+  x = tx * kTile + (blk & 7u) * 8u + (q & 7u);
+  y = ty * kTile + (blk >> 3) * 8u + (q >> 3);
+}
+
+// noise table of frame (batch frame fj) - back, back in {0, 1, 2}
+__device__ __forceinline__ const float4* noise_table(const BounceArgs& a, uint32_t fj, uint32_t back) {
+  return a.noise_window + (a.noise_offset + fj - back) * (kNoiseDim * kNoiseDim);
+}
+
 __device__ __forceinline__ uint32_t shade_noise_cell(uint32_t x, uint32_t y, uint32_t bounce, uint32_t f) {
   // renderer/Shaders.metal:135-136
   return ((x + bounce + f / 3) % kNoiseDim) + ((y + bounce + f / 5) % kNoiseDim) * kNoiseDim;
@@ -870,7 +889,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
 
   uint32_t N, in_chunk = 0;
   if (a.bounce == 0) {
-    N = a.num_slots;
+    N = a.num_slots * a.batch;
     __syncthreads();
   } else {
     for (uint32_t i = tid; i < nseg; i += kBlock) seg[i] = a.in_seg_count[i];
@@ -900,20 +919,18 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     const uint32_t idx = base + lane;
     bool active = idx < end;
     PathState s;
-    uint32_t tag = 0, slot = 0;   // tag = pixel | prevDiffuse << 31
+    uint32_t tag = 0, slot = 0;   // tag = global owned slot | prevDiffuse << 31
     if (active) {
       if (a.bounce == 0) {
-        // owned tile k -> global tile rank + k*count; 8x8 pixel blocks per wave
-        const uint32_t k = idx >> 12, p = idx & 4095u;
-        const uint32_t t = a.shard_rank + k * a.shard_count;
-        const uint32_t tx = t % a.tiles_x, ty = t / a.tiles_x;
-        const uint32_t blk = p >> 6, q = p & 63u;
-        const uint32_t x = tx * kTile + (blk & 7u) * 8u + (q & 7u);
-        const uint32_t y = ty * kTile + (blk >> 3) * 8u + (q >> 3);
+        // frame fj of the batch (num_slots is a multiple of 4096: waves never
+        // straddle frames, so fj is wave-uniform)
+        const uint32_t fj = a.batch == 1u ? 0u : __builtin_amdgcn_readfirstlane(idx / a.num_slots);
+        uint32_t x, y;
+        slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
         active = (x < a.width) && (y < a.height);
         if (active) {
-          tag = y * a.width + x;
-          const float4 ns = a.noise_raygen[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
+          tag = idx;
+          const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
           camera_ray(x, y, a.width, a.height, ns, s.o, s.d);
         }
       } else {
@@ -940,7 +957,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     STAMP(1);
     // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
     //    near hit ends the path (:122-126)
-    const uint32_t pix = tag & 0x7FFFFFFFu;
+    const uint32_t gslot = tag & 0x7FFFFFFFu;
     if (active && a.bounce == 0) {
       s.T = mk(1.0f, 1.0f, 1.0f);
       s.R = mk(0.0f, 0.0f, 0.0f);
@@ -952,8 +969,12 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     ShadowRay sh;
     sh.valid = false;
     if (hit_ok) {
-      const uint32_t y = pix / a.width, x = pix - y * a.width;
-      const float4 ns = a.noise_shade[shade_noise_cell(x, y, a.bounce, a.frame_index)];
+      uint32_t fj = 0;   // frame in batch: count of frame boundaries below gslot (no division)
+      for (uint32_t j = 1; j < a.batch; ++j) fj += gslot >= j * a.num_slots ? 1u : 0u;
+      uint32_t x, y;
+      slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+      const uint32_t back = (a.bounce % 3u) == 0 ? 0u : ((a.bounce % 3u) == 1 ? 2u : 1u);   // uniform
+      const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, a.bounce, a.frame_index + fj)];
       if (a.debug & 2u) {   // ablation: no shading, reflect back along the ray
         s.o = add(s.o, mul(s.d, h.t * 0.999f));
         s.d = mk(-s.d.x, -s.d.y, -s.d.z);
@@ -969,7 +990,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     STAMP(3);
     // -- phase 4: finished paths accumulate (accumulateImage, :233-249);
     //    survivors are compacted into this block's segment of the next queue
-    if (active && (!hit_ok || last)) a.radiance[pix] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
+    if (active && (!hit_ok || last)) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
     const bool alive = hit_ok && !last;
     const uint64_t mask = __ballot(alive);
     if (mask) {
@@ -978,7 +999,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
       wbase = __shfl(wbase, 0);
       if (alive && !(a.debug & 4u)) {
         const uint32_t o = out_base + wbase + (uint32_t)__popcll(mask & lanes_below);
-        a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(pix | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
+        a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
         a.out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
         a.out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
         a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
@@ -995,20 +1016,20 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   }
 }
 
-// accumulateImage (renderer/Shaders.metal:233-249) for one frame over the
-// owned tiles: image = f == 0 ? c : mix(c, image, f/(f+1)).  Frames are
-// accumulated strictly in order (the running mean is order-dependent).
+// accumulateImage (renderer/Shaders.metal:233-249) for a batch of frames over
+// the owned tiles: image = f == 0 ? c : mix(c, image, f/(f+1)).  Frames are
+// accumulated strictly in order (the running mean is order-dependent): one
+// thread applies the batch's frames to its pixel in frame order.
 __global__ __launch_bounds__(kBlock) void accumulate_frame_kernel(AccumArgs a) {
   for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < a.num_slots; idx += gridDim.x * kBlock) {
-    const uint32_t k = idx >> 12, p = idx & 4095u;
-    const uint32_t t = a.shard_rank + k * a.shard_count;
-    const uint32_t tx = t % a.tiles_x, ty = t / a.tiles_x;
-    // row-major inside the tile: consecutive lanes -> consecutive pixels
-    const uint32_t x = tx * kTile + (p & 63u), y = ty * kTile + (p >> 6);
+    uint32_t x, y;
+    slot_pixel(idx, a.shard_rank, a.shard_count, a.tiles_x, x, y);
     if (x >= a.width || y >= a.height) continue;
     const uint32_t pix = y * a.width + x;
-    const float4 c = a.radiance[pix];
-    accumulate_pixel(a.image, pix, mk(c), a.frame_index);
+    for (uint32_t j = 0; j < a.batch; ++j) {
+      const float4 c = a.radiance[j * a.num_slots + idx];
+      accumulate_pixel(a.image, pix, mk(c), a.frame_index + j);
+    }
   }
 }
 
@@ -1133,10 +1154,11 @@ size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_
 }
 
 // kTopLds: stage only as many top BVH nodes as keep the block's LDS within
-// 1/6 of the CU (the VGPR budget allows 6 resident blocks of 4 waves); the
-// BFS order makes any prefix the top levels.  Fewer staged nodes and full
-// occupancy beat more staged nodes (C4: 64 nodes 737 vs 128 nodes 715 Mpaths/s).
-constexpr size_t kLdsPerBlockTarget = 160 * 1024 / 6;
+// 1/6 of the CU less a 2-KB margin for allocation granularity (the VGPR
+// budget allows 6 resident blocks of 4 waves); the BFS order makes any prefix
+// the top levels.  Full occupancy beats more staged nodes: C4 with 80 nodes
+// 828, ~100 nodes (at the edge) 780, 128 nodes 715 Mpaths/s.
+constexpr size_t kLdsPerBlockTarget = 160 * 1024 / 6 - 2048;
 DeviceScene fit_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
   if (mode != kTopLds) return sc;
   DeviceScene f = sc;

@@ -110,8 +110,11 @@ struct mrt_renderer {
   // pending draw bookkeeping
   bool pending = false;
   uint32_t pending_frames = 0;
+  uint32_t pending_launches = 0;   // batches of the pending draw (bounce launches = batches * L)
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-  std::vector<hipEvent_t> kernel_events;   // MRT_FLAG_PROFILE: 2 per bounce launch
+  std::vector<hipEvent_t> kernel_events;   // MRT_FLAG_PROFILE: 2 per timed bounce launch
+  uint32_t profile_every = 8;
+  uint32_t batch = 1;                       // frames per bounce launch (frame batching)               // time the launches of every n-th frame (MRT_PROFILE_EVERY)
   size_t pending_events = 0;
   mrt_stats stats{};
   uint32_t stack_entries = 32;
@@ -126,35 +129,23 @@ int finalize_pending(mrt_renderer* r) {
   float ms = 0.0f;
   HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
   const uint32_t L = r->desc.max_path_length;
-  std::vector<uint32_t> cnt((size_t)r->pending_frames * L);
+  std::vector<uint32_t> cnt((size_t)r->pending_launches * L);
   HIP_TRY(hipMemcpy(cnt.data(), r->counters.p, cnt.size() * 4, hipMemcpyDeviceToHost));
-  uint64_t active = 0;
-  for (uint32_t f = 0; f < r->pending_frames; ++f) {
-    active += r->owned_pixels;                       // bounce 0: every owned pixel's camera ray
-    for (uint32_t b = 0; b + 1 < L; ++b) active += cnt[(size_t)f * L + b];
-  }
+  uint64_t active = r->owned_pixels * r->pending_frames;   // bounce 0: every owned pixel's camera ray
+  for (uint32_t k = 0; k < r->pending_launches; ++k)
+    for (uint32_t b = 0; b + 1 < L; ++b) active += cnt[(size_t)k * L + b];
   r->stats.active_ray_bounces += active;
   r->stats.last_draw_ms = ms;
   const uint64_t paths = r->owned_pixels * r->pending_frames;
   r->stats.mpaths_per_s = ms > 0.0f ? (double)paths / (ms * 1e-3) / 1e6 : 0.0;
+  r->stats.kernel_launches += (uint64_t)r->pending_launches * L;
   if (r->desc.flags & MRT_FLAG_PROFILE) {
-    std::vector<std::pair<float, float>> iv;   // launch intervals relative to the draw start
     for (size_t k = 0; k + 1 < r->pending_events; k += 2) {
-      float t0 = 0.0f, t1 = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&t0, r->ev_start, r->kernel_events[k]));
-      HIP_TRY(hipEventElapsedTime(&t1, r->ev_start, r->kernel_events[k + 1]));
-      r->stats.kernel_ms += t1 - t0;
-      r->stats.kernel_launches += 1;
-      iv.emplace_back(t0, t1);
+      float ms_k = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&ms_k, r->kernel_events[k], r->kernel_events[k + 1]));
+      r->stats.kernel_ms += ms_k;
+      r->stats.timed_launches += 1;
     }
-    std::sort(iv.begin(), iv.end());
-    double busy = 0.0, cur0 = -1.0, cur1 = -1.0;
-    for (const auto& x : iv) {
-      if (x.first > cur1) { if (cur1 > cur0) busy += cur1 - cur0; cur0 = x.first; cur1 = x.second; }
-      else cur1 = std::max<double>(cur1, x.second);
-    }
-    if (cur1 > cur0) busy += cur1 - cur0;
-    r->stats.kernel_busy_ms += busy;
   }
   r->pending = false;
   return MRT_OK;
@@ -166,7 +157,9 @@ int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
     mrt::make_noise_table(r->desc.seed, -1, t.data());
     HIP_TRY(upload(r->noise_init, t.data(), t.size() * 4));
   }
-  const int64_t lo = std::max<int64_t>(0, f0 - 2), hi = f0 + (int64_t)n;   // [lo, hi)
+  // window [f0 - 2, f0 + n): frames < 0 hold the initial table, so a kernel
+  // addresses T_{f - c} for every iteration without a select
+  const int64_t lo = f0 - 2, hi = f0 + (int64_t)n;
   if (r->noise_window.p && lo >= r->noise_first && hi <= r->noise_first + r->noise_count) return MRT_OK;
   const int64_t count = hi - lo;
   std::vector<float> host((size_t)count * mrt::kNoiseFloats);
@@ -175,7 +168,7 @@ int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
   for (unsigned t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
       for (int64_t k = t; k < count; k += nt)
-        mrt::make_noise_table(r->desc.seed, lo + k, host.data() + (size_t)k * mrt::kNoiseFloats);
+        mrt::make_noise_table(r->desc.seed, lo + k < 0 ? -1 : lo + k, host.data() + (size_t)k * mrt::kNoiseFloats);
     });
   for (auto& x : th) x.join();
   if (r->pending) { int rc = finalize_pending(r); if (rc) return rc; }
@@ -184,11 +177,6 @@ int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
   r->noise_first = lo;
   r->noise_count = count;
   return MRT_OK;
-}
-
-const float* noise_ptr(const mrt_renderer* r, int64_t frame) {
-  if (frame < 0) return r->noise_init.as<float>();
-  return r->noise_window.as<float>() + (size_t)(frame - r->noise_first) * mrt::kNoiseFloats;
 }
 
 int alloc_frame_buffers(mrt_renderer* r) {
@@ -205,14 +193,23 @@ int alloc_frame_buffers(mrt_renderer* r) {
     const uint64_t h = std::min<uint32_t>(mrt::kTile, H - ty * mrt::kTile);
     r->owned_pixels += w * h;
   }
-  // queue capacity: every owned slot + per-block rounding of the segments
-  const size_t slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096) + (size_t)r->grid * 256;
+  // frames per launch: enough to keep a launch near full-frame size when this
+  // GPU owns a small share of the tiles (2^21 rays ~ 1080p), at most kMaxBatch
+  const size_t owned_slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096);
+  r->batch = (uint32_t)std::min<size_t>(mrt::kMaxBatch, std::max<size_t>(1, ((size_t)1 << 21) / owned_slots));
+  if (const char* v = std::getenv("MRT_BATCH"))
+    r->batch = std::max<uint32_t>(1, std::min<uint32_t>(mrt::kMaxBatch, (uint32_t)std::strtoul(v, nullptr, 0)));
+  // a ray's tag holds batch * owned slots in 31 bits
+  while (r->batch > 1 && owned_slots * r->batch >= ((size_t)1 << 31)) --r->batch;
+  if (owned_slots >= ((size_t)1 << 31)) return fail(MRT_ERR_INVALID, "frame too large");
+  // queue capacity: every owned slot of the batch + per-block rounding of the segments
+  const size_t slots = owned_slots * r->batch + (size_t)r->grid * 256;
   for (FrameSlot& fs : r->slots) {
     HIP_TRY(fs.segments.alloc(((size_t)2 * r->grid + 2) * 4));
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(slots * 16));
-    HIP_TRY(fs.radiance.alloc((size_t)W * H * 16));
+    HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
     if (need > r->stack_entries && !fs.spill.p)
       HIP_TRY(fs.spill.alloc((size_t)(need - r->stack_entries) * r->grid * 256 * 4));
@@ -651,8 +648,10 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   r->stack_entries = want <= 8 ? 8 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
   if (need > r->stack_entries) r->stack_entries = r->stack_entries <= 8 ? 8 : r->stack_entries <= 16 ? 16 : 32;   // spill variants
   if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
+  if (const char* v = std::getenv("MRT_PROFILE_EVERY"))
+    r->profile_every = std::max<uint32_t>(1, (uint32_t)std::strtoul(v, nullptr, 0));
   if (const char* v = std::getenv("MRT_INFLIGHT")) r->inflight = (uint32_t)std::strtoul(v, nullptr, 0);
-  r->inflight = std::max<uint32_t>(1, std::min<uint32_t>(3, r->inflight));
+  r->inflight = std::max<uint32_t>(1, std::min<uint32_t>(8, r->inflight));
   r->slots.resize(r->inflight);
   for (uint32_t k = 0; k < r->inflight; ++k) {
     FrameSlot& fs = r->slots[k];
@@ -708,12 +707,14 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   rc = ensure_noise(r, (int64_t)r->frame_index, n);
   if (rc) return rc;
   const uint32_t L = r->desc.max_path_length;
-  const size_t counter_bytes = (size_t)n * L * 4;
+  const uint32_t B = r->batch;
+  const uint32_t nb = (n + B - 1) / B;   // launches of up to B frames each
+  const size_t counter_bytes = (size_t)nb * L * 4;
   if (r->counters.bytes < counter_bytes) HIP_TRY(r->counters.alloc(counter_bytes));
   HIP_TRY(hipMemsetAsync(r->counters.p, 0, counter_bytes, r->stream));
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
-    const size_t need = (size_t)2 * n * L;
+    const size_t need = (size_t)2 * ((nb + r->profile_every - 1) / r->profile_every) * L;
     while (r->kernel_events.size() < need) {
       hipEvent_t e;
       HIP_TRY(hipEventCreate(&e));
@@ -725,8 +726,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   uint32_t* cnt = r->counters.as<uint32_t>();
   size_t ev = 0;
   const FrameSlot* prev = nullptr;
-  for (uint32_t k = 0; k < n; ++k) {
-    const uint64_t f = r->frame_index + k;
+  for (uint32_t k = 0; k < nb; ++k) {
+    const uint64_t f = r->frame_index + (uint64_t)k * B;
+    const uint32_t batch = std::min<uint32_t>(B, n - k * B);
     FrameSlot& fs = r->slots[k % r->inflight];
     uint32_t* seg = fs.segments.as<uint32_t>();
     uint32_t* meta = seg + 2 * (size_t)r->grid;
@@ -735,6 +737,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.width = r->desc.width;
       a.height = r->desc.height;
       a.frame_index = (uint32_t)f;
+      a.batch = batch;
       a.bounce = b;
       a.max_path_length = L;
       a.shard_rank = r->desc.shard_rank;
@@ -752,20 +755,23 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
         a.in_q.plane[p] = fs.queue[b & 1][p].as<float4>();
         a.out_q.plane[p] = fs.queue[(b + 1) & 1][p].as<float4>();
       }
-      a.noise_raygen = reinterpret_cast<const float4*>(noise_ptr(r, (int64_t)f));
-      a.noise_shade = reinterpret_cast<const float4*>(noise_ptr(r, mrt::noise_frame_for_iteration((int64_t)f, b)));
+      a.noise_window = r->noise_window.as<float4>();
+      a.noise_offset = (uint32_t)((int64_t)f - r->noise_first);
       a.radiance = fs.radiance.as<float4>();
       a.stack_spill = fs.spill.as<uint32_t>();
-      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
+      const bool timed = profile && (k % r->profile_every) == 0;
+      if (timed) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
       HIP_TRY(launch_bounce(r, a, fs.stream));
-      if (profile) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
+      if (timed) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
     }
-    // accumulateImage for frame f, after frame f-1's (running mean order)
+    // accumulateImage for frames f .. f+batch-1, after the previous batch's
+    // (running mean order)
     if (prev && prev != &fs) HIP_TRY(hipStreamWaitEvent(fs.stream, prev->acc_done, 0));
     mrt::AccumArgs acc{};
     acc.width = r->desc.width;
     acc.height = r->desc.height;
     acc.frame_index = (uint32_t)f;
+    acc.batch = batch;
     acc.shard_rank = r->desc.shard_rank;
     acc.shard_count = r->desc.shard_count;
     acc.tiles_x = r->tiles_x;
@@ -777,10 +783,11 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     prev = &fs;
   }
   // join every slot back into the main stream
-  for (uint32_t k = 1; k < r->inflight && k < n; ++k) HIP_TRY(hipStreamWaitEvent(r->stream, r->slots[k].acc_done, 0));
+  for (uint32_t k = 1; k < r->inflight && k < nb; ++k) HIP_TRY(hipStreamWaitEvent(r->stream, r->slots[k].acc_done, 0));
   HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
   r->pending = true;
   r->pending_frames = n;
+  r->pending_launches = nb;
   r->pending_events = ev;
   r->frame_index += n;
   r->stats.frame_index = r->frame_index;

@@ -85,7 +85,7 @@ class Stats(ctypes.Structure):
         ("frame_index", ctypes.c_uint64), ("paths", ctypes.c_uint64), ("active_ray_bounces", ctypes.c_uint64),
         ("last_draw_ms", ctypes.c_double), ("mpaths_per_s", ctypes.c_double),
         ("kernel_launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("owned_pixels", ctypes.c_uint64),
-        ("kernel_busy_ms", ctypes.c_double),
+        ("timed_launches", ctypes.c_uint64),
     ]
 
     def as_dict(self):

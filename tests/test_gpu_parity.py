@@ -185,6 +185,27 @@ def test_shard_invariance(gpu, mrt_mod, shards):
     assert np.all(acc[..., 3] == 1.0)
 
 
+@pytest.mark.parametrize("scene", ["cornellbox", "CornellBox-Water-plastic"])
+def test_frame_batching_invariance(gpu, mrt_mod, monkeypatch, scene):
+    """Frames per launch (MRT_BATCH) and the split of frames across draw calls
+    change the launch structure, not the image: bitwise equal, same A."""
+    sc = _scene(mrt_mod, scene)
+    W, H, L = 136, 72, 5
+    out = {}
+    for batch, draws in [(1, (7,)), (3, (7,)), (8, (7,)), (3, (4, 3)), (2, (1, 5, 1))]:
+        monkeypatch.setenv("MRT_BATCH", str(batch))
+        r = mrt_mod.Renderer(sc, W, H, L, shard_rank=1, shard_count=2)
+        for d in draws:
+            r.draw(d)
+        out[(batch, draws)] = (r.read_image(), r.stats()["active_ray_bounces"])
+        r.close()
+    ref_img, ref_a = out[(1, (7,))]
+    assert np.isfinite(ref_img).all() and ref_img[..., :3].max() > 0
+    for key, (img, a) in out.items():
+        assert img.tobytes() == ref_img.tobytes(), key
+        assert a == ref_a, key
+
+
 def test_deterministic_and_reset(gpu, mrt_mod):
     sc = _scene(mrt_mod, "cornellbox")
     r = mrt_mod.Renderer(sc, 320, 240, 4)
