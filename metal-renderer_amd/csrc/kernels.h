@@ -32,6 +32,18 @@ struct RayQueue {
 // of the tiles still issues launches of full-frame size.
 constexpr uint32_t kMaxBatch = 8;
 
+// Dynamic work distribution inside a bounce launch: the dense input is split
+// into kGrabRanges contiguous ranges, each with its own grab counter (one
+// 128-B line apart, so the atomics do not serialise on one word); a wave
+// takes kGrab rays at a time from its home range, then steals from the next
+// ranges.  A block's output segment holds chunk + kSegSlack rays, where
+// kSegSlack >= (waves per block + 1) * kGrab keeps at least one block able to
+// grab until the input is exhausted (see bounce_kernel).
+constexpr uint32_t kGrab = 128;
+constexpr uint32_t kGrabRanges = 16;
+constexpr uint32_t kGrabStride = 32;    // uint32 words between counters
+constexpr uint32_t kSegSlack = 1024;
+
 struct BounceArgs {
   uint32_t width, height;
   uint32_t frame_index;        // SharedData.frameIndex of the batch's first frame
@@ -41,15 +53,17 @@ struct BounceArgs {
   uint32_t shard_rank, shard_count, tiles_x;
   uint32_t num_slots;          // per frame: owned tiles * 4096 pixel slots (bounce 0 input = num_slots * batch)
   uint32_t debug;              // ablation bits for profiling (0 in production, env MRT_DEBUG):
-                               //   1 = skip shadow traversal, 2 = skip shading, 4 = no queue writes
+                               //   1 = skip shadow traversal, 2 = skip shading, 4 = no queue writes,
+                               //   8 = static interleaved work assignment (no grab counters)
   // segmented queues: block g of a launch appends its survivors to slots
-  // [g*chunk, g*chunk + count_g) of the output queue
+  // [g*cap, g*cap + count_g) of the output queue (cap = chunk + kSegSlack)
   uint32_t in_segments;        // bounce > 0: number of input segments (previous grid size)
   const uint32_t* in_seg_count;
   const uint32_t* in_chunk;    // previous launch's chunk (segment stride in slots)
   uint32_t* out_seg_count;     // [grid]
   uint32_t* out_chunk;
   uint32_t* out_total;         // survivors of this launch (stats)
+  uint32_t* grab;              // [kGrabRanges * kGrabStride] zeroed grab counters of this launch
   RayQueue in_q, out_q;
   // noise: the table of frame g (T_g, or the initial table for g < 0) is
   // noise_window[(noise_offset + g - frame_index) * 4096 ...]; raygen reads
@@ -86,7 +100,8 @@ struct AccumArgs {
   hipError_t launch_accumulate(uint32_t W, uint32_t H, uint32_t frame_index, const RefRay* rays,          \
                                float* image, hipStream_t s);                                              \
   /* persistent grid size of the fused bounce kernel for this scene */                                    \
-  hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                 \
+  hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t blocks_per_cu,          \
+                         uint32_t* grid);                                                                \
   /* fused wavefront bounce over `grid` blocks (the same grid for every launch of a renderer);          \
      stack_entries = LDS stack capacity 8/16/24/32, deeper entries go to a.stack_spill */                 \
   hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \

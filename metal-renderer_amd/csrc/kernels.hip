@@ -35,11 +35,11 @@ constexpr int kBlock = 256;   // 4 waves of 64 lanes
 #else
 #define MRT_SHADE_BARRIER() do {} while (0)
 #endif
-// Minimum waves per SIMD for the bounce kernel (launch bounds): 6 caps it at
-// 80 VGPRs with a few scratch spills and measured +16 % over the 94-VGPR,
-// 4-wave allocation (traversal is latency-bound; occupancy hides it).
+// Minimum waves per SIMD for the bounce kernel (launch bounds): 5 caps it at
+// 96 VGPRs with 48 B/lane of scratch spills; 6 (80 VGPRs) spills ~140 B/lane
+// and 4 (no spills) hides less latency — 5 measured best with one stream.
 #ifndef MRT_BOUNCE_WAVES
-#define MRT_BOUNCE_WAVES 6
+#define MRT_BOUNCE_WAVES 5
 #endif
 
 // ---------------------------------------------------------------------------
@@ -879,13 +879,13 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n
 template <int STACK, int MODE, int WIDTH>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
-  __shared__ uint32_t s_cursor;
+  __shared__ uint32_t s_cursor, s_res;
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
   const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1, a.stack_spill);
   uint32_t* seg = lds_u32() + cx.scratch_base;   // exclusive prefix of the input segments
-  if (tid == 0) s_cursor = 0;
+  if (tid == 0) s_cursor = s_res = 0;
 
   uint32_t N, in_chunk = 0;
   if (a.bounce == 0) {
@@ -898,22 +898,61 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     in_chunk = *a.in_chunk;
   }
   const uint32_t chunk = ((N + G - 1) / G + kBlock - 1) / kBlock * kBlock;
-  const uint32_t begin = min(N, blockIdx.x * chunk), end = min(N, begin + chunk);
-  const uint32_t out_base = blockIdx.x * chunk;
-  // segments overlapping this block's range (narrow: segments are ~chunk long)
-  uint32_t seg_lo = 0, seg_hi = nseg;
-  if (nseg) {
-    uint32_t lo = 0, hi = nseg;   // last j with seg[j] <= begin
-    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= begin) lo = mid; else hi = mid; }
-    seg_lo = lo;
-  }
+  // Work assignment (see kernels.h): dynamic — waves grab kGrab rays at a
+  // time from kGrabRanges ranges, so the launch ends with at most one grab of
+  // imbalance instead of a tail of slow blocks; block output capacity
+  // cap = chunk + kSegSlack.  A wave reserves kGrab output slots in LDS
+  // before it grabs and returns what it did not use; a wave that cannot
+  // reserve stops.  A stopped block holds > cap - kGrab - 3*kGrab > chunk
+  // survivors, so not every block can stop while input remains (survivors
+  // <= N <= G*chunk): the input is always drained.
+  // MRT_DEBUG bit 8: static interleaved assignment (64-ray groups
+  // g*4 + w, + 4G, ...), capacity chunk.
+  const bool dynamic = (a.debug & 8u) == 0;
+  const uint32_t cap = dynamic ? chunk + kSegSlack : chunk;
+  const uint32_t out_base = blockIdx.x * cap;
+  const uint32_t rlen = ((N + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
+  uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
+  uint32_t static_base = blockIdx.x * kBlock + (tid & ~63u);
 
   const uint32_t lane = tid & 63u;
   const bool last = (a.bounce + 1 == a.max_path_length);
   const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
   STAMP_DECL();
-  for (uint32_t base = begin + (tid & ~63u); base < end; base += kBlock) {
+  for (;;) {
+    uint32_t start, end, niter;
+    if (dynamic) {
+      uint32_t got = 0xFFFFFFFFu;
+      if (lane == 0 && atomicAdd(&s_res, kGrab) + kGrab <= cap) {
+        while (ranges_left) {
+          const uint32_t r0 = cur_range * rlen;
+          if (r0 < N) {
+            const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
+            if (i < rlen && r0 + i < N) { got = r0 + i; break; }
+          }
+          cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
+          --ranges_left;
+        }
+        if (got == 0xFFFFFFFFu) atomicSub(&s_res, kGrab);
+      }
+      got = __builtin_amdgcn_readfirstlane(got);
+      if (got == 0xFFFFFFFFu) break;
+      cur_range = __builtin_amdgcn_readfirstlane(cur_range);
+      ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
+      start = got;
+      end = min(N, cur_range * rlen + rlen);
+      niter = kGrab / 64;
+    } else {
+      if (static_base >= N) break;
+      start = static_base;
+      end = N;
+      niter = 1;
+      static_base += G * kBlock;
+    }
+    uint32_t wrote = 0;
+    for (uint32_t it = 0; it < niter; ++it) {
+    const uint32_t base = start + it * 64u;
     STAMP_BEGIN();
     // -- phase 0: generate (bounce 0) or load (SoA queue planes 0-1) the ray
     const uint32_t idx = base + lane;
@@ -934,18 +973,16 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
           camera_ray(x, y, a.width, a.height, ns, s.o, s.d);
         }
       } else {
-        uint32_t lo = seg_lo, hi = seg_hi;   // last j with seg[j] <= idx
+        uint32_t lo = 0, hi = nseg;   // last j with seg[j] <= idx
         while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
         slot = lo * in_chunk + (idx - seg[lo]);
+        // planes 2-3 (throughput, pdf, radiance, ior) are loaded after the
+        // traversal: they are not needed there, and keeping them out of the
+        // traversal's live set saves 8 VGPRs
         const float4 q0 = a.in_q.plane[0][slot], q1 = a.in_q.plane[1][slot];
-        const float4 q2 = a.in_q.plane[2][slot], q3 = a.in_q.plane[3][slot];
         s.o = mk(q0);
         tag = fbits(q0.w);
         s.d = mk(q1);
-        s.T = mk(q2);
-        s.pdf = q2.w;
-        s.R = mk(q3);
-        s.ior = q3.w;
         s.prevDiffuse = (tag >> 31) ? 1.0f : 0.0f;
       }
     }
@@ -958,12 +995,20 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
     //    near hit ends the path (:122-126)
     const uint32_t gslot = tag & 0x7FFFFFFFu;
-    if (active && a.bounce == 0) {
-      s.T = mk(1.0f, 1.0f, 1.0f);
-      s.R = mk(0.0f, 0.0f, 0.0f);
-      s.pdf = 1.0f;
-      s.prevDiffuse = 0.0f;
-      s.ior = 1.00029f;
+    if (active) {
+      if (a.bounce == 0) {
+        s.T = mk(1.0f, 1.0f, 1.0f);
+        s.R = mk(0.0f, 0.0f, 0.0f);
+        s.pdf = 1.0f;
+        s.prevDiffuse = 0.0f;
+        s.ior = 1.00029f;
+      } else {
+        const float4 q2 = a.in_q.plane[2][slot], q3 = a.in_q.plane[3][slot];
+        s.T = mk(q2);
+        s.pdf = q2.w;
+        s.R = mk(q3);
+        s.ior = q3.w;
+      }
     }
     const bool hit_ok = active && h.found && !(h.t < kDistanceEpsilon);
     ShadowRay sh;
@@ -983,36 +1028,43 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
       }
     }
     STAMP(2);
-    // -- phase 3: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
-    if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE, WIDTH>(sc, cx, sh.o, sh.d, sh.target))) {
-      s.R = add(s.R, sh.L);
-    }
-    STAMP(3);
-    // -- phase 4: finished paths accumulate (accumulateImage, :233-249);
-    //    survivors are compacted into this block's segment of the next queue
+    // -- phase 3: paths that end here (miss, near hit, last bounce: none of
+    //    them carries a shadow ray) go to accumulateImage (:233-249);
+    //    survivors are compacted into this block's segment of the next queue.
+    //    Planes 0-2 are written before the shadow traversal so the next ray
+    //    is not live across it; plane 3 (radiance, ior) after it.
     if (active && (!hit_ok || last)) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
     const bool alive = hit_ok && !last;
     const uint64_t mask = __ballot(alive);
+    uint32_t o = 0;
     if (mask) {
       uint32_t wbase = 0;
       if (lane == 0) wbase = atomicAdd(&s_cursor, (uint32_t)__popcll(mask));
       wbase = __shfl(wbase, 0);
+      o = out_base + wbase + (uint32_t)__popcll(mask & lanes_below);
       if (alive && !(a.debug & 4u)) {
-        const uint32_t o = out_base + wbase + (uint32_t)__popcll(mask & lanes_below);
         a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
         a.out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
         a.out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
-        a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
       }
+      wrote += (uint32_t)__popcll(mask);
     }
+    STAMP(3);
+    // -- phase 4: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
+    if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE, WIDTH>(sc, cx, sh.o, sh.d, sh.target))) {
+      s.R = add(s.R, sh.L);
+    }
+    if (alive && !(a.debug & 4u)) a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
     STAMP(4);
+    }
+    if (dynamic && lane == 0) atomicSub(&s_res, kGrab - wrote);
   }
   STAMP_FLUSH();
   __syncthreads();
   if (tid == 0) {
     a.out_seg_count[blockIdx.x] = s_cursor;
     if (s_cursor) atomicAdd(a.out_total, s_cursor);   // stats: one atomic per block per launch
-    if (blockIdx.x == 0) *a.out_chunk = chunk;
+    if (blockIdx.x == 0) *a.out_chunk = cap;
   }
 }
 
@@ -1170,7 +1222,7 @@ DeviceScene fit_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack, uint3
 }
 
 template <int STACK, int MODE, int WIDTH>
-hipError_t grid_for(const DeviceScene& sc, uint32_t* grid) {
+hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* grid) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -1184,12 +1236,10 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t* grid) {
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bounce_kernel<STACK, MODE, WIDTH>, kBlock, lds) != hipSuccess || n <= 0)
     n = 1;
-  // LDS-resident scenes: 4 blocks per CU per launch — with several frames in
-  // flight the launches of different frames share the CUs, and a smaller grid
-  // shortens the per-block segment scan (measured best on C2 at 1 and 8
-  // shards).  Scenes traversed from global memory are latency-bound: 6 blocks
-  // per CU (C4 +6 %, C3 +2 % over 4).
-  *grid = (uint32_t)(prop.multiProcessorCount * std::min(n, MODE == kAllLds ? 4 : 6));
+  // one launch at a time: every resident block slot (the dynamic work
+  // distribution leaves no tail to fill); with frames in flight the caller
+  // asks for fewer blocks per CU per launch
+  *grid = (uint32_t)(prop.multiProcessorCount * (blocks_per_cu ? std::min<uint32_t>(n, blocks_per_cu) : n));
   return hipSuccess;
 }
 
@@ -1206,11 +1256,11 @@ hipError_t dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32_t gr
                          hipStream_t s) {
   switch (choose_mode(sc)) {
     case kAllLds:
-      return a ? launch_bounce_t<STACK, kAllLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kAllLds, WIDTH>(sc, grid_out);
+      return a ? launch_bounce_t<STACK, kAllLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kAllLds, WIDTH>(sc, grid, grid_out);
     case kTopLds:
-      return a ? launch_bounce_t<STACK, kTopLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kTopLds, WIDTH>(sc, grid_out);
+      return a ? launch_bounce_t<STACK, kTopLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kTopLds, WIDTH>(sc, grid, grid_out);
     default:
-      return a ? launch_bounce_t<STACK, kGlobal, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kGlobal, WIDTH>(sc, grid_out);
+      return a ? launch_bounce_t<STACK, kGlobal, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kGlobal, WIDTH>(sc, grid, grid_out);
   }
 }
 
@@ -1298,8 +1348,9 @@ hipError_t read_stamps(unsigned long long* out8, bool reset) {
 #endif
 }
 
-hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid) {
-  return dispatch(sc, nullptr, stack_entries, 0, grid, nullptr);
+hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t blocks_per_cu, uint32_t* grid) {
+  // (dispatch passes `grid` through as blocks_per_cu when no launch is given)
+  return dispatch(sc, nullptr, stack_entries, blocks_per_cu, grid, nullptr);
 }
 
 hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,

@@ -100,8 +100,10 @@ struct mrt_renderer {
   uint32_t tiles_x = 0, tiles_y = 0, owned_tiles = 0;
   uint64_t owned_pixels = 0;
   std::vector<FrameSlot> slots;
-  uint32_t inflight = 3;   // frames in flight (MRT_INFLIGHT); 1 -> 2 measured +47 % on C2
+  uint32_t inflight = 1;   // frames in flight (MRT_INFLIGHT): with dynamic work distribution and
+                           // 8-frame batches one stream is as fast as 3 (C2) and launches do not overlap
   DevBuf counters;          // per (frame, bounce) survivor totals (stats)
+  DevBuf grabs;             // per (launch) grab counters of the dynamic work distribution
   uint32_t grid = 0;        // persistent grid of the bounce kernel
   // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
   DevBuf noise_init, noise_window;
@@ -193,17 +195,19 @@ int alloc_frame_buffers(mrt_renderer* r) {
     const uint64_t h = std::min<uint32_t>(mrt::kTile, H - ty * mrt::kTile);
     r->owned_pixels += w * h;
   }
-  // frames per launch: enough to keep a launch near full-frame size when this
-  // GPU owns a small share of the tiles (2^21 rays ~ 1080p), at most kMaxBatch
+  // frames per launch: about 2^24 rays per launch (8 frames at 1080p), so
+  // the launch-boundary drain is a small share of each launch and a GPU that
+  // owns a small share of the tiles still issues full-size launches
   const size_t owned_slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096);
-  r->batch = (uint32_t)std::min<size_t>(mrt::kMaxBatch, std::max<size_t>(1, ((size_t)1 << 21) / owned_slots));
+  r->batch = (uint32_t)std::min<size_t>(mrt::kMaxBatch, std::max<size_t>(1, ((size_t)1 << 24) / owned_slots));
   if (const char* v = std::getenv("MRT_BATCH"))
     r->batch = std::max<uint32_t>(1, std::min<uint32_t>(mrt::kMaxBatch, (uint32_t)std::strtoul(v, nullptr, 0)));
   // a ray's tag holds batch * owned slots in 31 bits
   while (r->batch > 1 && owned_slots * r->batch >= ((size_t)1 << 31)) --r->batch;
   if (owned_slots >= ((size_t)1 << 31)) return fail(MRT_ERR_INVALID, "frame too large");
-  // queue capacity: every owned slot of the batch + per-block rounding of the segments
-  const size_t slots = owned_slots * r->batch + (size_t)r->grid * 256;
+  // queue capacity: every owned slot of the batch + per-block rounding and
+  // slack of the segments (kernels.h)
+  const size_t slots = owned_slots * r->batch + (size_t)r->grid * (256 + mrt::kSegSlack);
   for (FrameSlot& fs : r->slots) {
     HIP_TRY(fs.segments.alloc(((size_t)2 * r->grid + 2) * 4));
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
@@ -663,8 +667,8 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     }
     HIP_TRY(hipEventCreateWithFlags(&fs.acc_done, hipEventDisableTiming));
   }
-  HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, &r->grid)
-                                           : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, &r->grid));
+  HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid)
+                                           : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid));
   if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
   int rc = alloc_frame_buffers(r.get());
   if (rc) return rc;
@@ -712,6 +716,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   const size_t counter_bytes = (size_t)nb * L * 4;
   if (r->counters.bytes < counter_bytes) HIP_TRY(r->counters.alloc(counter_bytes));
   HIP_TRY(hipMemsetAsync(r->counters.p, 0, counter_bytes, r->stream));
+  const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
+  if (r->grabs.bytes < (size_t)nb * L * grab_words * 4) HIP_TRY(r->grabs.alloc((size_t)nb * L * grab_words * 4));
+  HIP_TRY(hipMemsetAsync(r->grabs.p, 0, (size_t)nb * L * grab_words * 4, r->stream));
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
     const size_t need = (size_t)2 * ((nb + r->profile_every - 1) / r->profile_every) * L;
@@ -751,6 +758,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.out_seg_count = seg + (size_t)(b & 1) * r->grid;
       a.out_chunk = meta + (b & 1);
       a.out_total = cnt + (size_t)k * L + b;
+      a.grab = r->grabs.as<uint32_t>() + ((size_t)k * L + b) * grab_words;
       for (int p = 0; p < 4; ++p) {
         a.in_q.plane[p] = fs.queue[b & 1][p].as<float4>();
         a.out_q.plane[p] = fs.queue[(b + 1) & 1][p].as<float4>();
