@@ -54,7 +54,8 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--precise", action="store_true", help="time the parity build instead of the fast build")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-frames", type=int, default=8, help="frames of the workload timed on the CPU oracle")
+    p.add_argument("--cpu-frames", type=int, default=0,
+                   help="frames of the workload timed on the CPU oracle (default: all spp frames for C2, 8 otherwise)")
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="N=1 only: time rank 0's tiles of an S-way tile split (one GPU's share)")
@@ -63,10 +64,24 @@ def parse():
     return p.parse_args()
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg, frames):
-    """The CPU oracle (scalar C++ restatement, oracle/) on a bounded sample of
-    the same workload: `frames` frames over a row band sized so the sample is
-    ~10-30 s of CPU work, std::thread over rows (brute-force nearest hit)."""
+    """The CPU oracle (scalar C++ restatement of the path, oracle/; brute-force
+    nearest hit in place of MPS) timed on this host on a bounded sample of the
+    same workload: C2 runs in full (all `frames` = spp frames
+    of the whole image) on `threads` std::threads over rows, and 2 frames on
+    one thread give the scalar rate.  Scenes with more triangles run a row
+    band sized to keep the sample within ~10-30 s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle  # test/baseline infrastructure only (see oracle/mrt_oracle.cpp header)
@@ -87,10 +102,17 @@ def cpu_baseline(cfg, frames):
     sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads, pixel_mask=mask)
     dt = time.perf_counter() - t0
     paths = W * rows * frames
+    f1 = min(2, frames)
+    t1 = time.perf_counter()
+    sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, f1, threads=1, pixel_mask=mask)
+    dt1 = time.perf_counter() - t1
     return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "single_thread_value": round(W * rows * f1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
+            "cpu_model": _cpu_model(),
             "sample": f"frames 0-{frames - 1}, rows {y0}-{y0 + rows - 1} of the workload ({W}x{rows} of {W}x{H}, "
                       f"L={cfg['L']}, {paths} paths), brute-force nearest hit over {sc.n_triangles} triangles, "
-                      f"{threads} std::threads over rows, {dt:.2f} s wall"}
+                      f"{threads} std::threads over rows, {dt:.2f} s wall; single thread: frames 0-{f1 - 1} "
+                      f"of the same rows, {dt1:.2f} s"}
 
 
 def main():
@@ -223,7 +245,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames)
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames or (spp if args.config == "c2" else 8))
     if rank == 0:
         print(json.dumps(result), flush=True)
     r.close()
