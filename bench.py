@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--precise", action="store_true", help="time the parity build instead of the fast build")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"],
+                   help="BVH builder: host binned SAH (default) or the device LBVH (MRT_BVH_DEVICE_LBVH)")
     p.add_argument("--cpu-frames", type=int, default=0,
                    help="frames of the workload timed on the CPU oracle (default: all spp frames for C2, 8 otherwise)")
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
@@ -141,7 +143,8 @@ def main():
         else:
             dist.init_process_group("gloo")
     W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
-    scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=device)
+    scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=device,
+                      bvh_builder=mrt.BVH_DEVICE_LBVH if args.bvh == "lbvh" else mrt.BVH_HOST_SAH)
     # the accumulation image lives in a torch tensor so RCCL can reduce it in
     # place; libmrt renders into it on its own stream (torch ships its own HIP
     # runtime copy, so streams are not shared: r.sync() orders the reduce)
@@ -234,7 +237,10 @@ def main():
         "config": {"workload": cfg["workload"], "width": W, "height": H, "spp": spp, "max_path_length": L,
                    "scene": cfg["scene"], "parallelism": (f"tile shard 0 of {shard_count} (one GPU's share)" if args.shard_of else
                                    f"tiles64x{world}" + (" + rccl reduce" if world > 1 else "")),
-                   "build": "precise" if args.precise else "fast"},
+                   "build": "precise" if args.precise else "fast",
+                   "bvh": {"builder": "device-lbvh" if args.bvh == "lbvh" else "host-sah",
+                           "build_ms": round(scene.info["build_ms"], 2), "nodes": scene.info["bvh_nodes"],
+                           "max_stack": scene.info["bvh_max_stack"]}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),

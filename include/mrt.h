@@ -18,6 +18,9 @@
  *        MPS nearest-hit     (Renderer.mm:519-523,545-553; config :464-469)
  *                                                     -> mrt_intersect
  *        MPS rebuild         (Renderer.mm:456-462)    -> mrt_scene_create (BVH build)
+ *   MPS itself, over raw vertex/index buffers (Renderer.mm:456-469):
+ *        MPSTriangleAccelerationStructure + rebuild -> mrt_accel_create / mrt_accel_rebuild
+ *        MPSRayIntersector encodeIntersection (Nearest)  -> mrt_accel_intersect
  *        intersectionHandler (Shaders.metal:105-212)  -> mrt_shade
  *        lightSamplingHandler(Shaders.metal:214-231)  -> mrt_resolve_shadow
  *        accumulateImage     (Shaders.metal:233-249)  -> mrt_accumulate
@@ -41,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 2
+#define MRT_ABI_VERSION 3
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -70,7 +73,13 @@ typedef struct mrt_scene_desc {
   uint32_t lds_nodes;              /* top BVH nodes staged in LDS, 0 = default; UINT32_MAX = none */
   int device;                      /* HIP device ordinal; -1 = host only (import + BVH, no upload) */
   uint32_t bvh_width;              /* 2 = BVH2, 4 = BVH4 (collapsed BVH2), 0 = default (4) */
+  uint32_t bvh_builder;            /* MRT_BVH_*; 0 = default (host binned SAH) */
 } mrt_scene_desc;
+
+/* BVH builders */
+#define MRT_BVH_HOST_SAH 1u      /* host binned-SAH BVH2, collapsed to BVH4 (best traversal quality) */
+#define MRT_BVH_DEVICE_LBVH 2u   /* device linear BVH (Morton sort + radix tree, collapsed to BVH4
+                                    on the GPU; BVH4 only) — builds from device buffers, no host copy */
 
 typedef struct mrt_scene_info {
   uint32_t vertices, triangles, materials, light_triangles;
@@ -93,6 +102,38 @@ int mrt_scene_destroy(mrt_scene* scene);
  * leaf, every child box contains its subtree's triangles, depth within the
  * traversal stack.  0 = valid. */
 int mrt_scene_check_bvh(const mrt_scene* scene);
+
+/* ---- acceleration structure over raw buffers (the MPS interface) --------
+ * MPSTriangleAccelerationStructure (Renderer.mm:456-462): vertexBuffer with
+ * vertexStride = sizeof(Vertex) = 24, uint32 indexBuffer, triangleCount =
+ * indices / 3, `rebuild` once; MPSRayIntersector (Renderer.mm:464-469):
+ * nearest hit, cull none, ray records (origin, minDistance, direction,
+ * maxDistance) at rayStride, intersections (distance, primitiveIndex, (u,v)). */
+typedef struct mrt_accel mrt_accel;
+typedef struct mrt_accel_desc {
+  const void* vertices;            /* device pointer: 3 floats (position) at the start of every vertex */
+  uint32_t vertex_stride;          /* bytes between vertices (>= 12, multiple of 4) */
+  const uint32_t* indices;         /* device pointer: 3 uint32 per triangle */
+  uint32_t triangle_count;
+  int device;                      /* HIP device of the buffers */
+  uint32_t builder;                /* MRT_BVH_*; 0 = default (MRT_BVH_DEVICE_LBVH) */
+  uint32_t max_leaf_size;          /* 0 = default (4) */
+  void* stream;                    /* hipStream_t of libmrt's runtime, NULL = own stream */
+} mrt_accel_desc;
+typedef struct mrt_accel_info {
+  uint32_t triangles, bvh_nodes, bvh_leaves, bvh_levels, bvh_max_stack, builder;
+  double build_ms;                 /* device time (LBVH) or host time (SAH) of the last (re)build */
+  uint64_t device_bytes;
+} mrt_accel_info;
+/* Build the structure (the buffers must stay valid until the next rebuild). */
+int mrt_accel_create(const mrt_accel_desc* desc, mrt_accel** out);
+/* Rebuild from the same buffers (their contents may have changed). */
+int mrt_accel_rebuild(mrt_accel* accel);
+/* Nearest hit of `count` ray records of `stride` bytes (contract of mrt_intersect). */
+int mrt_accel_intersect(const mrt_accel* accel, const void* rays, uint32_t stride, uint32_t count,
+                        void* intersections, uint32_t flags, void* stream);
+int mrt_accel_info_get(const mrt_accel* accel, mrt_accel_info* info);
+int mrt_accel_destroy(mrt_accel* accel);
 
 /* ---- stage-level ABI (B-2), reference AoS layouts, device pointers ------- */
 /* rayGenerator over a W x H grid: noise = 64*64 float4 (one noise slot). */

@@ -77,7 +77,7 @@ constexpr int32_t kEmptyChild = 0x7FFFFFFF;
 constexpr int kLeafCountBits = 4;
 constexpr int kMaxLeafSize = 1 << kLeafCountBits;   // 16
 constexpr int kMaxBvhDepth = 32;                    // builder forces leaves below this binary depth
-constexpr int kMaxStack = 48;                       // traversal stack entries per ray (BVH4 bound < 1.5 x depth)
+constexpr int kMaxStack = 64;                       // traversal stack entries per ray (host SAH BVH4 < 1.5 x depth; device LBVH deeper)
 
 // Device-resident scene, passed to kernels by value.  Every pointer is
 // 16-B aligned device memory; float pointers documented as "float4" hold

@@ -24,6 +24,7 @@
 
 #include "../../include/mrt.h"
 #include "bvh.h"
+#include "bvh_gpu.h"
 #include "kernels.h"
 #include "noise.h"
 #include "scene.h"
@@ -65,6 +66,14 @@ hipError_t upload(DevBuf& b, const void* src, size_t n) {
 }
 
 }  // namespace
+
+// MPS-shaped acceleration structure over caller-owned device buffers
+struct mrt_accel {
+  mrt_accel_desc desc{};
+  DevBuf nodes, tris;
+  mrt::DeviceScene dev{};
+  mrt_accel_info info{};
+};
 
 struct mrt_scene {
   int device = 0;
@@ -389,10 +398,46 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   opt.width = desc->bvh_width ? desc->bvh_width : 4;
   if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
   if (opt.width != 2 && opt.width != 4) return fail(MRT_ERR_INVALID, "bvh_width must be 2 or 4");
-  const auto t0 = std::chrono::steady_clock::now();
-  if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), h.indices.data(), T, opt, s->bvh, err))
-    return fail(MRT_ERR_INVALID, "BVH build failed: " + err);
-  const double build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
+  if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH) return fail(MRT_ERR_INVALID, "unknown bvh_builder");
+  if (builder == MRT_BVH_DEVICE_LBVH && desc->device < 0) return fail(MRT_ERR_INVALID, "device BVH build needs a device");
+  if (builder == MRT_BVH_DEVICE_LBVH && opt.width != 4) return fail(MRT_ERR_INVALID, "device BVH build is BVH4 only");
+  double build_ms = 0.0;
+  if (builder == MRT_BVH_HOST_SAH) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), h.indices.data(), T, opt, s->bvh, err))
+      return fail(MRT_ERR_INVALID, "BVH build failed: " + err);
+    build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  } else {
+    // MPS-style: the vertex and index buffers go to the device first and the
+    // structure is built there (MPSTriangleAccelerationStructure.rebuild)
+    HIP_TRY(hipSetDevice(desc->device));
+    DevBuf dv, di;
+    HIP_TRY(upload(dv, h.vertices.data(), h.vertices.size() * sizeof(mrt::RefVertex)));
+    HIP_TRY(upload(di, h.indices.data(), h.indices.size() * 4));
+    mrt::GpuBvhResult g;
+    if (mrt::build_bvh_gpu(dv.as<float>(), sizeof(mrt::RefVertex), di.as<uint32_t>(), T, opt.max_leaf_size, nullptr, g,
+                           err) != hipSuccess)
+      return fail(MRT_ERR_HIP, "device BVH build failed: " + err);
+    s->nodes.p = g.nodes; s->nodes.bytes = g.nodes_bytes;
+    s->tris.p = g.tris; s->tris.bytes = g.tris_bytes;
+    build_ms = g.build_ms;
+    // host copy of the tree for mrt_scene_check_bvh / info
+    mrt::BvhResult& b = s->bvh;
+    b.nodes.resize(g.nodes_bytes / 4);
+    b.tris.resize(g.tris_bytes / 4);
+    HIP_TRY(hipMemcpy(b.nodes.data(), g.nodes, g.nodes_bytes, hipMemcpyDeviceToHost));
+    if (g.tris_bytes) HIP_TRY(hipMemcpy(b.tris.data(), g.tris, g.tris_bytes, hipMemcpyDeviceToHost));
+    b.root = g.root;
+    b.num_nodes = g.num_nodes;
+    b.num_leaves = g.num_leaves;
+    b.max_depth = g.levels;
+    b.wide_depth = g.levels;
+    b.width = 4;
+    b.max_stack = g.max_stack;
+    b.lds_nodes = std::min<uint32_t>(opt.lds_node_budget, g.num_nodes);   // BFS order: any prefix is the top
+    b.sah_cost = 0.0;
+  }
   if (s->bvh.max_stack > (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack");
 
   // per-primitive shading records (primitive order)
@@ -446,8 +491,10 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     return MRT_OK;
   }
   HIP_TRY(hipSetDevice(desc->device));
-  HIP_TRY(upload(s->nodes, s->bvh.nodes.data(), s->bvh.nodes.size() * 4));
-  HIP_TRY(upload(s->tris, s->bvh.tris.data(), s->bvh.tris.size() * 4));
+  if (builder == MRT_BVH_HOST_SAH) {
+    HIP_TRY(upload(s->nodes, s->bvh.nodes.data(), s->bvh.nodes.size() * 4));
+    HIP_TRY(upload(s->tris, s->bvh.tris.data(), s->bvh.tris.size() * 4));
+  }
   HIP_TRY(upload(s->prims, prims.data(), prims.size() * 4));
   HIP_TRY(upload(s->materials, mats.data(), mats.size() * 4));
   HIP_TRY(upload(s->lights, lights.data(), lights.size() * 4));
@@ -564,6 +611,124 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
 
 int mrt_scene_destroy(mrt_scene* scene) {
   delete scene;
+  return MRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// acceleration structure over raw buffers (MPSTriangleAccelerationStructure +
+// MPSRayIntersector, renderer/Renderer.mm:456-469)
+// ---------------------------------------------------------------------------
+namespace {
+int accel_build(mrt_accel* a) {
+  const mrt_accel_desc& d = a->desc;
+  const uint32_t T = d.triangle_count;
+  const uint32_t leaf = d.max_leaf_size ? d.max_leaf_size : 4;
+  HIP_TRY(hipSetDevice(d.device));
+  hipStream_t s = (hipStream_t)d.stream;
+  std::string err;
+  if (a->info.builder == MRT_BVH_DEVICE_LBVH) {
+    mrt::GpuBvhResult g;
+    if (mrt::build_bvh_gpu(reinterpret_cast<const float*>(d.vertices), d.vertex_stride, d.indices, T, leaf, s, g,
+                           err) != hipSuccess)
+      return fail(MRT_ERR_HIP, "device BVH build failed: " + err);
+    (void)a->nodes.alloc(0);
+    (void)a->tris.alloc(0);
+    a->nodes.p = g.nodes; a->nodes.bytes = g.nodes_bytes;
+    a->tris.p = g.tris; a->tris.bytes = g.tris_bytes;
+    a->dev.root = g.root;
+    a->dev.num_nodes = g.num_nodes;
+    a->dev.max_stack = g.max_stack;
+    a->info.bvh_nodes = g.num_nodes;
+    a->info.bvh_leaves = g.num_leaves;
+    a->info.bvh_levels = g.levels;
+    a->info.bvh_max_stack = g.max_stack;
+    a->info.build_ms = g.build_ms;
+  } else {
+    // host binned SAH: read the buffers back (the reference's own data path
+    // never does this; kept for quality comparison and as a fallback-free
+    // alternative for small scenes)
+    HIP_TRY(hipStreamSynchronize(s));
+    uint32_t nv = 0;
+    std::vector<uint32_t> idx((size_t)T * 3);
+    if (T) HIP_TRY(hipMemcpy(idx.data(), d.indices, idx.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t v : idx) nv = std::max(nv, v + 1);
+    std::vector<uint8_t> verts((size_t)nv * d.vertex_stride);
+    if (nv) HIP_TRY(hipMemcpy(verts.data(), d.vertices, verts.size(), hipMemcpyDeviceToHost));
+    mrt::BvhBuildOptions opt;
+    opt.max_leaf_size = leaf;
+    opt.width = 4;
+    opt.lds_node_budget = 0;
+    mrt::BvhResult b;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (T == 0) return fail(MRT_ERR_INVALID, "host SAH build of an empty structure (use the device builder)");
+    if (!mrt::build_bvh(reinterpret_cast<const float*>(verts.data()), d.vertex_stride, idx.data(), T, opt, b, err))
+      return fail(MRT_ERR_INVALID, "BVH build failed: " + err);
+    a->info.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    HIP_TRY(upload(a->nodes, b.nodes.data(), b.nodes.size() * 4));
+    HIP_TRY(upload(a->tris, b.tris.data(), b.tris.size() * 4));
+    a->dev.root = b.root;
+    a->dev.num_nodes = b.num_nodes;
+    a->dev.max_stack = b.max_stack;
+    a->info.bvh_nodes = b.num_nodes;
+    a->info.bvh_leaves = b.num_leaves;
+    a->info.bvh_levels = b.wide_depth;
+    a->info.bvh_max_stack = b.max_stack;
+  }
+  if (a->dev.max_stack > (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack");
+  a->dev.nodes = a->nodes.as<float>();
+  a->dev.tris = a->tris.as<float>();
+  a->dev.num_triangles = T;
+  a->dev.width = 4;
+  a->dev.lds_nodes = 0;
+  a->info.triangles = T;
+  a->info.device_bytes = a->nodes.bytes + a->tris.bytes;
+  return MRT_OK;
+}
+}  // namespace
+
+int mrt_accel_create(const mrt_accel_desc* desc, mrt_accel** out) {
+  if (!desc || !out) return fail(MRT_ERR_INVALID, "mrt_accel_create: null argument");
+  *out = nullptr;
+  if (desc->triangle_count && (!desc->vertices || !desc->indices))
+    return fail(MRT_ERR_INVALID, "mrt_accel_create: null buffer");
+  if (desc->vertex_stride < 12 || desc->vertex_stride % 4) return fail(MRT_ERR_INVALID, "mrt_accel_create: bad vertex_stride");
+  if (desc->max_leaf_size > (uint32_t)mrt::kMaxLeafSize) return fail(MRT_ERR_INVALID, "mrt_accel_create: max_leaf_size > 16");
+  const uint32_t builder = desc->builder ? desc->builder : MRT_BVH_DEVICE_LBVH;
+  if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH) return fail(MRT_ERR_INVALID, "unknown builder");
+  std::unique_ptr<mrt_accel> a(new mrt_accel());
+  a->desc = *desc;
+  a->info.builder = builder;
+  const int rc = accel_build(a.get());
+  if (rc) return rc;
+  *out = a.release();
+  return MRT_OK;
+}
+
+int mrt_accel_rebuild(mrt_accel* accel) {
+  if (!accel) return fail(MRT_ERR_INVALID, "null accel");
+  return accel_build(accel);
+}
+
+int mrt_accel_intersect(const mrt_accel* accel, const void* rays, uint32_t stride, uint32_t count, void* isect,
+                        uint32_t flags, void* stream) {
+  if (!accel || (!rays && count) || (!isect && count) || stride < 32 || (stride % 4))
+    return fail(MRT_ERR_INVALID, "mrt_accel_intersect: bad argument");
+  HIP_TRY(hipSetDevice(accel->desc.device));
+  if (precise(flags))
+    HIP_TRY(mrt::precise::launch_intersect(accel->dev, rays, stride, count, (mrt::RefIntersection*)isect, (hipStream_t)stream));
+  else
+    HIP_TRY(mrt::fast::launch_intersect(accel->dev, rays, stride, count, (mrt::RefIntersection*)isect, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+int mrt_accel_info_get(const mrt_accel* accel, mrt_accel_info* info) {
+  if (!accel || !info) return fail(MRT_ERR_INVALID, "null argument");
+  *info = accel->info;
+  return MRT_OK;
+}
+
+int mrt_accel_destroy(mrt_accel* accel) {
+  delete accel;
   return MRT_OK;
 }
 

@@ -54,6 +54,27 @@ class SceneDesc(ctypes.Structure):
         ("lds_nodes", ctypes.c_uint32),
         ("device", ctypes.c_int),
         ("bvh_width", ctypes.c_uint32),
+        ("bvh_builder", ctypes.c_uint32),
+    ]
+
+
+BVH_HOST_SAH, BVH_DEVICE_LBVH = 1, 2
+
+
+class AccelDesc(ctypes.Structure):
+    _fields_ = [
+        ("vertices", ctypes.c_void_p), ("vertex_stride", ctypes.c_uint32),
+        ("indices", ctypes.c_void_p), ("triangle_count", ctypes.c_uint32),
+        ("device", ctypes.c_int), ("builder", ctypes.c_uint32), ("max_leaf_size", ctypes.c_uint32),
+        ("stream", ctypes.c_void_p),
+    ]
+
+
+class AccelInfo(ctypes.Structure):
+    _fields_ = [
+        ("triangles", ctypes.c_uint32), ("bvh_nodes", ctypes.c_uint32), ("bvh_leaves", ctypes.c_uint32),
+        ("bvh_levels", ctypes.c_uint32), ("bvh_max_stack", ctypes.c_uint32), ("builder", ctypes.c_uint32),
+        ("build_ms", ctypes.c_double), ("device_bytes", ctypes.c_uint64),
     ]
 
 
@@ -100,6 +121,7 @@ EXPORTED = [
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
     "mrt_debug_stamps", "mrt_shard_mask",
+    "mrt_accel_create", "mrt_accel_rebuild", "mrt_accel_intersect", "mrt_accel_info_get", "mrt_accel_destroy",
 ]
 
 _lib = None
@@ -148,6 +170,11 @@ def lib() -> ctypes.CDLL:
         "mrt_synchronize": [vp],
         "mrt_debug_stamps": [vp, c_int],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
+        "mrt_accel_create": [ctypes.POINTER(AccelDesc), ctypes.POINTER(vp)],
+        "mrt_accel_rebuild": [vp],
+        "mrt_accel_intersect": [vp, vp, u32, u32, vp, u32, vp],
+        "mrt_accel_info_get": [vp, ctypes.POINTER(AccelInfo)],
+        "mrt_accel_destroy": [vp],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -173,10 +200,10 @@ class Scene:
 
     def __init__(self, obj: str, mtl_override: str | None = None, *, procedural_triangles: int = 0,
                  procedural_seed: int = 1, max_leaf_size: int = 0, lds_nodes: int = 0, device: int = 0,
-                 bvh_width: int = 0):
+                 bvh_width: int = 0, bvh_builder: int = 0):
         self._h = None
         d = SceneDesc(scene_path(obj).encode(), (mtl_override or "").encode(), procedural_triangles,
-                      procedural_seed, max_leaf_size, lds_nodes, device, bvh_width)
+                      procedural_seed, max_leaf_size, lds_nodes, device, bvh_width, bvh_builder)
         h = ctypes.c_void_p()
         _check(lib().mrt_scene_create(ctypes.byref(d), ctypes.byref(h)), "mrt_scene_create")
         self._h = h
@@ -215,6 +242,47 @@ class Scene:
     def close(self):
         if self._h:
             lib().mrt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Accel:
+    """MPSTriangleAccelerationStructure + MPSRayIntersector over caller-owned
+    device buffers (renderer/Renderer.mm:456-469): positions at `vertex_stride`
+    (24 = sizeof(Vertex)), uint32 indices, nearest-hit queries."""
+
+    def __init__(self, vertices_ptr: int, vertex_stride: int, indices_ptr: int, triangle_count: int, *,
+                 device: int = 0, builder: int = 0, max_leaf_size: int = 0, stream: int | None = None):
+        self._h = None
+        d = AccelDesc(vertices_ptr, vertex_stride, indices_ptr, triangle_count, device, builder, max_leaf_size,
+                      stream)
+        h = ctypes.c_void_p()
+        _check(lib().mrt_accel_create(ctypes.byref(d), ctypes.byref(h)), "mrt_accel_create")
+        self._h = h
+
+    def rebuild(self) -> None:
+        _check(lib().mrt_accel_rebuild(self._h), "mrt_accel_rebuild")
+
+    def info(self) -> dict:
+        i = AccelInfo()
+        _check(lib().mrt_accel_info_get(self._h, ctypes.byref(i)), "mrt_accel_info_get")
+        return {k: getattr(i, k) for k, _ in AccelInfo._fields_}
+
+    def intersect(self, rays_ptr: int, stride: int, count: int, isect_ptr: int, precise=True, stream=None,
+                  sync=True) -> None:
+        _check(lib().mrt_accel_intersect(self._h, rays_ptr, stride, count, isect_ptr, _flags(precise), stream),
+               "mrt_accel_intersect")
+        if sync:
+            synchronize(stream)
+
+    def close(self):
+        if self._h:
+            lib().mrt_accel_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(mrt_mod):
     missing = [n for n in sorted(declared) if not hasattr(lib, n)]
     assert not missing, missing
     assert set(mrt_mod.EXPORTED) == declared
-    assert mrt_mod.lib().mrt_abi_version() == 2
+    assert mrt_mod.lib().mrt_abi_version() == 3
 
 
 def test_device_count_never_fails(mrt_mod):
@@ -133,3 +133,20 @@ def test_errors_are_status_codes(mrt_mod):
     assert b"null" in L.mrt_last_error()
     with pytest.raises(mrt_mod.MrtError, match="shard_rank"):
         mrt_mod.shard_mask(64, 64, 3, 2)
+
+
+def test_accel_argument_errors(mrt_mod):
+    """mrt_accel_* validate their arguments before touching a device."""
+    import ctypes
+    L = mrt_mod.lib()
+    h = ctypes.c_void_p()
+    assert L.mrt_accel_create(None, ctypes.byref(h)) == -1
+    d = mrt_mod.AccelDesc(None, 24, None, 12, 0, 0, 0, None)   # triangles but no buffers
+    assert L.mrt_accel_create(ctypes.byref(d), ctypes.byref(h)) == -1 and b"null buffer" in L.mrt_last_error()
+    d = mrt_mod.AccelDesc(1, 8, 1, 12, 0, 0, 0, None)           # stride below one position
+    assert L.mrt_accel_create(ctypes.byref(d), ctypes.byref(h)) == -1 and b"vertex_stride" in L.mrt_last_error()
+    d = mrt_mod.AccelDesc(1, 24, 1, 12, 0, 7, 0, None)          # unknown builder
+    assert L.mrt_accel_create(ctypes.byref(d), ctypes.byref(h)) == -1 and b"builder" in L.mrt_last_error()
+    assert L.mrt_accel_intersect(None, None, 80, 0, None, 0, None) == -1
+    with pytest.raises(mrt_mod.MrtError, match="needs a device"):
+        mrt_mod.Scene("cornellbox", device=-1, bvh_builder=mrt_mod.BVH_DEVICE_LBVH)

@@ -174,5 +174,56 @@ int main(int argc, char** argv) {
                 pass ? "secondary" : "camera", steps / rays, inner / rays, leaves / rays, tris / rays,
                 lane_iters / wave_iters);
   }
+  // ray-sorting model: secondary rays in pixel-block order, then stably
+  // sorted by a direction key inside windows of S rays; efficiency of waves
+  {
+    struct R { V o, d; int key; int steps; };
+    std::vector<R> rs;
+    std::mt19937 rng2(7);
+    for (uint32_t by = 0; by + 8 <= H; by += 8)
+      for (uint32_t bx = 0; bx + 8 <= W; bx += 8)
+        for (uint32_t q = 0; q < 64; ++q) {
+          uint32_t x = bx + (q & 7), y = by + (q >> 3);
+          float ncx = 2.0f * x / (W - 1) - 1.0f, ncy = (2.0f * y / (H - 1) - 1.0f) * H / W;
+          V d = {ncx, ncy, -1.0f};
+          float l = std::sqrt(dot(d, d));
+          d = {d.x / l, d.y / l, d.z / l};
+          V o = {0.0f, 1.0f, 2.35f};
+          Counts c = trace(b, o, d);
+          if (!std::isfinite(c.t)) continue;
+          V h = {o.x + d.x * c.t * 0.999f, o.y + d.y * c.t * 0.999f, o.z + d.z * c.t * 0.999f};
+          V r;
+          do { r = {2 * U(rng2) - 1, 2 * U(rng2) - 1, 2 * U(rng2) - 1}; } while (dot(r, r) > 1 || dot(r, r) < 1e-4f);
+          float rl = std::sqrt(dot(r, r));
+          r = {r.x / rl, r.y / rl, r.z / rl};
+          if (dot(r, d) > 0) r = {-r.x, -r.y, -r.z};
+          R rr{h, r, 0, trace(b, h, r).steps};
+          rs.push_back(rr);
+        }
+    for (int keybits : {0, 3, 6}) {
+      for (size_t S : {size_t(128), size_t(1024), size_t(8192), rs.size()}) {
+        std::vector<R> v = rs;
+        for (R& x : v) {
+          int k = (x.d.x > 0) | ((x.d.y > 0) << 1) | ((x.d.z > 0) << 2);
+          if (keybits == 6) {   // octant + dominant axis + half
+            float ax = std::fabs(x.d.x), ay = std::fabs(x.d.y), az = std::fabs(x.d.z);
+            int dom = ax >= ay && ax >= az ? 0 : (ay >= az ? 1 : 2);
+            k = k * 8 + dom * 2 + (std::max(ax, std::max(ay, az)) > 0.8f);
+          }
+          x.key = keybits ? k : 0;
+        }
+        for (size_t w0 = 0; w0 < v.size(); w0 += S)
+          std::stable_sort(v.begin() + w0, v.begin() + std::min(v.size(), w0 + S), [](const R& a, const R& c) { return a.key < c.key; });
+        double li = 0, wi = 0;
+        for (size_t w0 = 0; w0 < v.size(); w0 += 64) {
+          int mx = 0;
+          for (size_t i = w0; i < std::min(v.size(), w0 + 64); ++i) { li += v[i].steps; mx = std::max(mx, v[i].steps); }
+          wi += 64.0 * mx;
+        }
+        std::printf("sorted secondaries: key bits %d window %zu: SIMD efficiency %.3f\n", keybits, S, li / wi);
+        if (!keybits) break;
+      }
+    }
+  }
   return 0;
 }
