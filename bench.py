@@ -61,6 +61,10 @@ def parse():
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="N=1 only: time rank 0's tiles of an S-way tile split (one GPU's share)")
+    p.add_argument("--exchange", default="gather", choices=["gather", "reduce"],
+                   help="N>1 image exchange: RCCL gather of packed owned tiles (default) or SUM reduce of the image")
+    p.add_argument("--check-image", action="store_true",
+                   help="N>1: rank 0 renders the frame alone afterwards and asserts the exchanged image is bitwise equal")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="gloo = rehearsal of the N>1 path on fewer GPUs (reduce on a host copy)")
     return p.parse_args()
@@ -154,16 +158,43 @@ def main():
                      image_ptr=image.data_ptr())
     r.prepare(spp)
 
-    def step():
-        r.reset()
-        r.draw(spp)
-        if world > 1:
-            r.sync()
+    # multi-GPU exchange: every rank's owned 64x64 tiles go
+    # to rank 0 — by default one RCCL gather of the densely packed tiles
+    # (1/N of the image per rank), or one RCCL SUM reduce of the whole image
+    # (non-owned pixels are 0); both give the 1-GPU image bitwise
+    packed_n = mrt.tiles_packed_floats(W, H, 0, world) if world > 1 else 0   # rank 0 owns the most tiles
+    if world > 1:
+        tdev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        packed = torch.zeros(packed_n, dtype=torch.float32, device="cuda")
+        gathered = [torch.zeros(packed_n, dtype=torch.float32, device=tdev) for _ in range(world)] if rank == 0 else None
+        torch.cuda.synchronize()
+
+    def exchange():
+        r.sync()
+        if args.exchange == "reduce":
             if args.dist_backend == "nccl":
                 dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
             else:
                 host = image.cpu()
                 dist.reduce(host, dst=0)
+                if rank == 0:
+                    image.copy_(host.cuda())
+                    torch.cuda.synchronize()
+            return
+        mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed.data_ptr())   # libmrt runtime, synchronised
+        src = packed if args.dist_backend == "nccl" else packed.cpu()
+        dist.gather(src, gathered, dst=0)   # the single RCCL gather of the packed tiles (xGMI)
+        if rank == 0:
+            torch.cuda.synchronize()
+            for k in range(1, world):
+                g = gathered[k] if args.dist_backend == "nccl" else gathered[k].cuda()
+                mrt.tiles_unpack(g.data_ptr(), W, H, k, world, image.data_ptr(), sync=(k == world - 1))
+
+    def step():
+        r.reset()
+        r.draw(spp)
+        if world > 1:
+            exchange()
 
     for _ in range(args.warmup):
         step()
@@ -236,7 +267,7 @@ def main():
                 ", deterministic noise seed",
         "config": {"workload": cfg["workload"], "width": W, "height": H, "spp": spp, "max_path_length": L,
                    "scene": cfg["scene"], "parallelism": (f"tile shard 0 of {shard_count} (one GPU's share)" if args.shard_of else
-                                   f"tiles64x{world}" + (" + rccl reduce" if world > 1 else "")),
+                                   f"tiles64x{world}" + (f" + rccl {args.exchange}" if world > 1 else "")),
                    "build": "precise" if args.precise else "fast",
                    "bvh": {"builder": "device-lbvh" if args.bvh == "lbvh" else "host-sah",
                            "build_ms": round(scene.info["build_ms"], 2), "nodes": scene.info["bvh_nodes"],
@@ -252,6 +283,18 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames or (spp if args.config == "c2" else 8))
+    if world > 1 and args.check_image:
+        if rank == 0:   # the exchanged image == one device rendering the whole frame, bitwise
+            ref = torch.zeros_like(image)
+            torch.cuda.synchronize()
+            r1 = mrt.Renderer(scene, W, H, L, precise=args.precise, image_ptr=ref.data_ptr())
+            r1.draw(spp)
+            r1.sync()
+            r1.close()
+            same = bool(torch.equal(ref.view(-1, 4)[:, :3], image.view(-1, 4)[:, :3]))
+            result["image_check"] = "bitwise equal to the 1-GPU render" if same else "MISMATCH"
+            assert same, "exchanged image differs from the single-device render"
+        dist.barrier()
     if rank == 0:
         print(json.dumps(result), flush=True)
     r.close()

@@ -216,6 +216,18 @@ int mrt_noise_table(uint64_t seed, int64_t frame, float* out16384);
  * (row 0 = bottom); returns the number of owned pixels via *owned. */
 int mrt_shard_mask(uint32_t width, uint32_t height, uint32_t shard_rank, uint32_t shard_count, uint8_t* mask,
                    uint64_t* owned);
+/* Multi-GPU exchange of the accumulation image: a shard's
+ * owned 64x64 tiles packed densely, [k][64*64] RGBA32F for its k-th owned
+ * tile (tile t = shard_rank + k*shard_count, row-major tiles; zeros outside
+ * the image).  Device pointers; pack reads `image`, unpack writes only the
+ * shard's pixels of `image`.  Bitwise moves.  mrt_tiles_packed_floats gives
+ * the packed size (host, no device). */
+int mrt_tiles_packed_floats(uint32_t width, uint32_t height, uint32_t shard_rank, uint32_t shard_count,
+                            uint64_t* floats);
+int mrt_tiles_pack(const float* image, uint32_t width, uint32_t height, uint32_t shard_rank,
+                   uint32_t shard_count, float* packed, void* stream);
+int mrt_tiles_unpack(const float* packed, uint32_t width, uint32_t height, uint32_t shard_rank,
+                     uint32_t shard_count, float* image, void* stream);
 /* Wait for work queued by libmrt on `stream` (NULL = everything on the device
  * libmrt's runtime has queued). */
 int mrt_synchronize(void* stream);

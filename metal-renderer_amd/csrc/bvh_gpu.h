@@ -3,8 +3,8 @@
 // (renderer/Renderer.mm:456-462), which builds from the GPU-resident
 // vertex/index buffers without a host round trip.
 //
-// Linear BVH (Karras 2012): 30-bit Morton codes of the triangle centroids,
-// one device radix sort (rocPRIM) of (code, triangle) keys, the binary radix
+// Linear BVH (Karras 2012): 63-bit Morton codes of the triangle centroids,
+// one device radix sort (rocPRIM) of (code, triangle) pairs, the binary radix
 // tree built in one pass (one thread per internal node), boxes refitted
 // bottom-up with arrival counters, then a level-synchronous top-down collapse
 // into the BVH4 node layout of mrt_layout.h (largest-area child opened first,

@@ -64,17 +64,19 @@ __global__ __launch_bounds__(kB) void k_centroid_bounds(const uint8_t* pos, uint
   }
 }
 
-__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {   // 10 bits -> every third bit
-  v = (v * 0x00010001u) & 0xFF0000FFu;
-  v = (v * 0x00000101u) & 0x0F00F00Fu;
-  v = (v * 0x00000011u) & 0xC30C30C3u;
-  v = (v * 0x00000005u) & 0x49249249u;
-  return v;
+__device__ __forceinline__ uint64_t split3(uint32_t a) {   // 21 bits -> every third bit of 63
+  uint64_t x = a & 0x1FFFFFu;
+  x = (x | x << 32) & 0x1F00000000FFFFull;
+  x = (x | x << 16) & 0x1F0000FF0000FFull;
+  x = (x | x << 8) & 0x100F00F00F00F00Full;
+  x = (x | x << 4) & 0x10C30C30C30C30C3ull;
+  x = (x | x << 2) & 0x1249249249249249ull;
+  return x;
 }
 
-// key = 30-bit Morton code of the centroid << 32 | triangle: all keys distinct
+// 63-bit Morton code of the centroid (21 bits per axis) + triangle index
 __global__ __launch_bounds__(kB) void k_morton(const uint8_t* pos, uint32_t stride, const uint32_t* idx, uint32_t T,
-                                               const uint32_t* bounds, uint64_t* keys) {
+                                               const uint32_t* bounds, uint64_t* keys, uint32_t* vals) {
   const uint32_t t = blockIdx.x * kB + threadIdx.x;
   if (t >= T) return;
   const float3 c = centroid(load_tri(pos, stride, idx, t));
@@ -84,18 +86,20 @@ __global__ __launch_bounds__(kB) void k_morton(const uint8_t* pos, uint32_t stri
     const float lo = o2f(bounds[k]), hi = o2f(bounds[3 + k]);
     const float ext = hi - lo;
     const float u = ext > 0.0f ? (cc[k] - lo) / ext : 0.0f;
-    q[k] = (uint32_t)fminf(fmaxf(u * 1024.0f, 0.0f), 1023.0f);
+    q[k] = (uint32_t)fminf(fmaxf(u * 2097152.0f, 0.0f), 2097151.0f);
   }
-  const uint32_t m = (expand_bits(q[0]) << 2) | (expand_bits(q[1]) << 1) | expand_bits(q[2]);
-  keys[t] = ((uint64_t)m << 32) | t;
+  keys[t] = (split3(q[0]) << 2) | (split3(q[1]) << 1) | split3(q[2]);
+  vals[t] = t;
 }
 
 // Binary radix tree over the sorted keys (Karras 2012): one thread per
 // internal node i in [0, T-2].  child refs: >= 0 internal, < 0 leaf ~p
-// (p = sorted position).
+// (p = sorted position).  Equal codes are told apart by their sorted
+// position (the augmented common prefix of Karras §4).
 __device__ __forceinline__ int delta(const uint64_t* k, int n, int a, int b) {
   if (b < 0 || b >= n) return -1;
-  return __clzll(k[a] ^ k[b]);
+  const uint64_t x = k[a] ^ k[b];
+  return x ? __clzll(x) : 64 + __clz((uint32_t)(a ^ b));
 }
 __global__ __launch_bounds__(kB) void k_radix_tree(const uint64_t* keys, int n, int32_t* child, int32_t* parent_int,
                                                    int32_t* parent_leaf, uint32_t* rfirst, uint32_t* rcount) {
@@ -132,13 +136,13 @@ __global__ __launch_bounds__(kB) void k_radix_tree(const uint64_t* keys, int n, 
 // box from both children.  Release/acquire at agent scope around the
 // counter makes the sibling's box visible across XCDs.
 __global__ __launch_bounds__(kB) void k_leaves_refit(const uint8_t* pos, uint32_t stride, const uint32_t* idx,
-                                                     const uint64_t* keys, uint32_t T, const int32_t* child,
+                                                     const uint32_t* order, uint32_t T, const int32_t* child,
                                                      const int32_t* parent_int, const int32_t* parent_leaf,
                                                      float4* tris, float4* leaf_box, float4* node_box,
                                                      uint32_t* arrivals, bool climb) {
   const uint32_t p = blockIdx.x * kB + threadIdx.x;
   if (p >= T) return;
-  const uint32_t t = (uint32_t)(keys[p] & 0xFFFFFFFFu);
+  const uint32_t t = order[p];
   const Tri3 v = load_tri(pos, stride, idx, t);
   tris[3 * (size_t)p + 0] = make_float4(v.a.x, v.a.y, v.a.z, __uint_as_float(t));
   tris[3 * (size_t)p + 1] = make_float4(v.b.x - v.a.x, v.b.y - v.a.y, v.b.z - v.a.z, 0.0f);
@@ -296,13 +300,13 @@ hipError_t build_bvh_gpu(const float* positions, uint32_t stride_bytes, const ui
   if (T <= max_leaf) {
     // tiny scene: one node whose single child is the leaf of every triangle
     // (or no child at all for an empty scene)
-    Tmp keys, lbox;
-    GB_TRY(keys.alloc((size_t)T * 8));
+    Tmp order, lbox;
+    GB_TRY(order.alloc((size_t)T * 4));
     GB_TRY(lbox.alloc((size_t)T * 32));
-    std::vector<uint64_t> hk(T);
-    for (uint32_t t = 0; t < T; ++t) hk[t] = t;
-    if (T) GB_TRY(hipMemcpyAsync(keys.p, hk.data(), (size_t)T * 8, hipMemcpyHostToDevice, s));
-    if (T) k_leaves_refit<<<blocks, kB, 0, s>>>(pos, stride_bytes, indices, keys.as<uint64_t>(), T, nullptr, nullptr,
+    std::vector<uint32_t> ho(T);
+    for (uint32_t t = 0; t < T; ++t) ho[t] = t;
+    if (T) GB_TRY(hipMemcpyAsync(order.p, ho.data(), (size_t)T * 4, hipMemcpyHostToDevice, s));
+    if (T) k_leaves_refit<<<blocks, kB, 0, s>>>(pos, stride_bytes, indices, order.as<uint32_t>(), T, nullptr, nullptr,
                                                 nullptr, reinterpret_cast<float4*>(out.tris), lbox.as<float4>(),
                                                 nullptr, nullptr, false);
     GB_TRY(hipGetLastError());
@@ -336,22 +340,27 @@ hipError_t build_bvh_gpu(const float* positions, uint32_t stride_bytes, const ui
     out.num_nodes = 1;
     out.levels = 1;
   } else {
-    Tmp bounds, keys, keys_sorted, child, pint, pleaf, rfirst, rcount, lbox, nbox, arr, sort_tmp, fr_node[2],
+    Tmp bounds, keys, keys_sorted, vals, vals_sorted, child, pint, pleaf, rfirst, rcount, lbox, nbox, arr, sort_tmp, fr_node[2],
         fr_need[2], counters;
     GB_TRY(bounds.alloc(24));
     const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
     GB_TRY(hipMemcpyAsync(bounds.p, init, 24, hipMemcpyHostToDevice, s));
     GB_TRY(keys.alloc((size_t)T * 8));
     GB_TRY(keys_sorted.alloc((size_t)T * 8));
+    GB_TRY(vals.alloc((size_t)T * 4));
+    GB_TRY(vals_sorted.alloc((size_t)T * 4));
     const uint32_t nb = std::min<uint32_t>(blocks, 4096);
     k_centroid_bounds<<<nb, kB, 0, s>>>(pos, stride_bytes, indices, T, bounds.as<uint32_t>());
     GB_TRY(hipGetLastError());
-    k_morton<<<blocks, kB, 0, s>>>(pos, stride_bytes, indices, T, bounds.as<uint32_t>(), keys.as<uint64_t>());
+    k_morton<<<blocks, kB, 0, s>>>(pos, stride_bytes, indices, T, bounds.as<uint32_t>(), keys.as<uint64_t>(),
+                                   vals.as<uint32_t>());
     GB_TRY(hipGetLastError());
     size_t tmp_bytes = 0;
-    GB_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, keys.as<uint64_t>(), keys_sorted.as<uint64_t>(), T, 0, 62, s));
+    GB_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, keys.as<uint64_t>(), keys_sorted.as<uint64_t>(),
+                                     vals.as<uint32_t>(), vals_sorted.as<uint32_t>(), T, 0, 63, s));
     GB_TRY(sort_tmp.alloc(tmp_bytes));
-    GB_TRY(rocprim::radix_sort_keys(sort_tmp.p, tmp_bytes, keys.as<uint64_t>(), keys_sorted.as<uint64_t>(), T, 0, 62, s));
+    GB_TRY(rocprim::radix_sort_pairs(sort_tmp.p, tmp_bytes, keys.as<uint64_t>(), keys_sorted.as<uint64_t>(),
+                                     vals.as<uint32_t>(), vals_sorted.as<uint32_t>(), T, 0, 63, s));
     GB_TRY(child.alloc((size_t)(T - 1) * 8));
     GB_TRY(pint.alloc((size_t)(T - 1) * 4));
     GB_TRY(pleaf.alloc((size_t)T * 4));
@@ -365,7 +374,7 @@ hipError_t build_bvh_gpu(const float* positions, uint32_t stride_bytes, const ui
     GB_TRY(nbox.alloc((size_t)(T - 1) * 32));
     GB_TRY(arr.alloc((size_t)(T - 1) * 4));
     GB_TRY(hipMemsetAsync(arr.p, 0, (size_t)(T - 1) * 4, s));
-    k_leaves_refit<<<blocks, kB, 0, s>>>(pos, stride_bytes, indices, keys_sorted.as<uint64_t>(), T,
+    k_leaves_refit<<<blocks, kB, 0, s>>>(pos, stride_bytes, indices, vals_sorted.as<uint32_t>(), T,
                                          child.as<int32_t>(), pint.as<int32_t>(), pleaf.as<int32_t>(),
                                          reinterpret_cast<float4*>(out.tris), lbox.as<float4>(), nbox.as<float4>(),
                                          arr.as<uint32_t>(), true);

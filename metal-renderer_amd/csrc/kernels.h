@@ -28,9 +28,10 @@ struct RayQueue {
 };
 
 // Frame batching: one launch carries the rays of `batch` consecutive frames
-// (frame_index .. frame_index + batch - 1), so a GPU that owns a small share
-// of the tiles still issues launches of full-frame size.
-constexpr uint32_t kMaxBatch = 8;
+// (frame_index .. frame_index + batch - 1): about 2^24 rays per launch, so a
+// GPU that owns a small share of the tiles (1/8 of 1080p: 64 frames per
+// launch) still issues launches of the same size as a whole 1080p GPU.
+constexpr uint32_t kMaxBatch = 64;
 
 // Dynamic work distribution inside a bounce launch: the dense input is split
 // into kGrabRanges contiguous ranges, each with its own grab counter (one
@@ -108,6 +109,10 @@ struct AccumArgs {
                            uint32_t grid, hipStream_t s);                                                 \
   /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \
   hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s);                                  \
+  /* owned-tile exchange: pack a shard's tiles of a W x H RGBA32F image into                             \
+     [owned tile][64 x 64] float4 (zeros outside the image), or unpack them back (bitwise moves) */     \
+  hipError_t launch_tiles_move(const float4* src, float4* dst, uint32_t W, uint32_t H, uint32_t rank,    \
+                               uint32_t count, bool pack, hipStream_t s);                                 \
   /* diagnostic phase stamps (MRT_STAMPS builds; zeros otherwise) */                                      \
   hipError_t read_stamps(unsigned long long* out8, bool reset);                                          \
   }

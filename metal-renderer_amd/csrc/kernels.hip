@@ -1016,8 +1016,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     ShadowRay sh;
     sh.valid = false;
     if (hit_ok) {
-      uint32_t fj = 0;   // frame in batch: count of frame boundaries below gslot (no division)
-      for (uint32_t j = 1; j < a.batch; ++j) fj += gslot >= j * a.num_slots ? 1u : 0u;
+      const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;   // frame in batch
       uint32_t x, y;
       slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
       const uint32_t back = (a.bounce % 3u) == 0 ? 0u : ((a.bounce % 3u) == 1 ? 2u : 1u);   // uniform
@@ -1334,6 +1333,34 @@ hipError_t launch_accumulate(uint32_t W, uint32_t H, uint32_t frame_index, const
 hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s) {
   const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks_for(a.num_slots), 4096));
   accumulate_frame_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(a);
+  return hipGetLastError();
+}
+
+// owned-tile pack/unpack for the multi-GPU exchange (renderer.cpp
+// mrt_tiles_pack / mrt_tiles_unpack): packed index = k * 4096 + ty * 64 + tx
+// for the k-th owned tile (global tile rank + k * count, row-major tiles)
+__global__ __launch_bounds__(kBlock) void tiles_move_kernel(const float4* src, float4* dst, uint32_t W, uint32_t H,
+                                                            uint32_t rank, uint32_t count, uint32_t tiles_x,
+                                                            uint32_t owned, bool pack) {
+  const uint64_t n = (uint64_t)owned * kTile * kTile;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t k = (uint32_t)(i >> 12), p = (uint32_t)(i & 4095u);
+    const uint32_t t = rank + k * count;
+    const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+    const uint32_t x = tx * kTile + (p & 63u), y = ty * kTile + (p >> 6);
+    const bool in = x < W && y < H;
+    if (pack) dst[i] = in ? src[(size_t)y * W + x] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    else if (in) dst[(size_t)y * W + x] = src[i];
+  }
+}
+
+hipError_t launch_tiles_move(const float4* src, float4* dst, uint32_t W, uint32_t H, uint32_t rank, uint32_t count,
+                             bool pack, hipStream_t s) {
+  const uint32_t tx = (W + kTile - 1) / kTile, ty = (H + kTile - 1) / kTile, T = tx * ty;
+  const uint32_t owned = rank < T ? (T - rank + count - 1) / count : 0u;
+  if (!owned) return hipSuccess;
+  const uint32_t blocks = std::min<uint32_t>(4096u, owned * 16u);
+  tiles_move_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(src, dst, W, H, rank, count, tx, owned, pack);
   return hipGetLastError();
 }
 

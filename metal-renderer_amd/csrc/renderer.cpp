@@ -204,9 +204,11 @@ int alloc_frame_buffers(mrt_renderer* r) {
     const uint64_t h = std::min<uint32_t>(mrt::kTile, H - ty * mrt::kTile);
     r->owned_pixels += w * h;
   }
-  // frames per launch: about 2^24 rays per launch (8 frames at 1080p), so
-  // the launch-boundary drain is a small share of each launch and a GPU that
-  // owns a small share of the tiles still issues full-size launches
+  // frames per launch: about 2^24 rays per launch (8 frames at 1080p, 64
+  // frames of a 1/8 tile share), so the launch-boundary drain is a small share
+  // of each launch and a GPU that owns a small share of the tiles still
+  // issues full-size launches (1/8 share with 8-frame batches: 62 % of the
+  // per-GPU rate)
   const size_t owned_slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096);
   r->batch = (uint32_t)std::min<size_t>(mrt::kMaxBatch, std::max<size_t>(1, ((size_t)1 << 24) / owned_slots));
   if (const char* v = std::getenv("MRT_BATCH"))
@@ -349,6 +351,33 @@ int mrt_shard_mask(uint32_t W, uint32_t H, uint32_t rank, uint32_t count, uint8_
     }
   (void)ty_n;
   if (owned) *owned = n;
+  return MRT_OK;
+}
+
+int mrt_tiles_packed_floats(uint32_t W, uint32_t H, uint32_t rank, uint32_t count, uint64_t* floats) {
+  const uint32_t S = count ? count : 1;
+  if (!floats || W == 0 || H == 0 || rank >= S) return fail(MRT_ERR_INVALID, "mrt_tiles_packed_floats: bad argument");
+  const uint32_t T = ((W + mrt::kTile - 1) / mrt::kTile) * ((H + mrt::kTile - 1) / mrt::kTile);
+  const uint64_t owned = rank < T ? (T - rank + S - 1) / S : 0;
+  *floats = owned * mrt::kTile * mrt::kTile * 4;
+  return MRT_OK;
+}
+
+int mrt_tiles_pack(const float* image, uint32_t W, uint32_t H, uint32_t rank, uint32_t count, float* packed,
+                   void* stream) {
+  const uint32_t S = count ? count : 1;
+  if (!image || !packed || W == 0 || H == 0 || rank >= S) return fail(MRT_ERR_INVALID, "mrt_tiles_pack: bad argument");
+  HIP_TRY(mrt::fast::launch_tiles_move(reinterpret_cast<const float4*>(image), reinterpret_cast<float4*>(packed), W, H,
+                                       rank, S, true, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+int mrt_tiles_unpack(const float* packed, uint32_t W, uint32_t H, uint32_t rank, uint32_t count, float* image,
+                     void* stream) {
+  const uint32_t S = count ? count : 1;
+  if (!image || !packed || W == 0 || H == 0 || rank >= S) return fail(MRT_ERR_INVALID, "mrt_tiles_unpack: bad argument");
+  HIP_TRY(mrt::fast::launch_tiles_move(reinterpret_cast<const float4*>(packed), reinterpret_cast<float4*>(image), W, H,
+                                       rank, S, false, (hipStream_t)stream));
   return MRT_OK;
 }
 

@@ -121,6 +121,7 @@ EXPORTED = [
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
     "mrt_debug_stamps", "mrt_shard_mask",
+    "mrt_tiles_packed_floats", "mrt_tiles_pack", "mrt_tiles_unpack",
     "mrt_accel_create", "mrt_accel_rebuild", "mrt_accel_intersect", "mrt_accel_info_get", "mrt_accel_destroy",
 ]
 
@@ -170,6 +171,9 @@ def lib() -> ctypes.CDLL:
         "mrt_synchronize": [vp],
         "mrt_debug_stamps": [vp, c_int],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
+        "mrt_tiles_packed_floats": [u32, u32, u32, u32, ctypes.POINTER(u64)],
+        "mrt_tiles_pack": [vp, u32, u32, u32, u32, vp, vp],
+        "mrt_tiles_unpack": [vp, u32, u32, u32, u32, vp, vp],
         "mrt_accel_create": [ctypes.POINTER(AccelDesc), ctypes.POINTER(vp)],
         "mrt_accel_rebuild": [vp],
         "mrt_accel_intersect": [vp, vp, u32, u32, vp, u32, vp],
@@ -424,6 +428,50 @@ def shard_mask(width: int, height: int, rank: int, count: int):
     _check(lib().mrt_shard_mask(width, height, rank, count, ctypes.c_void_p(m.ctypes.data),
                                 ctypes.c_void_p(n.ctypes.data)), "mrt_shard_mask")
     return m, int(n[0])
+
+
+def tiles_packed_floats(width: int, height: int, rank: int, count: int) -> int:
+    n = ctypes.c_uint64()
+    _check(lib().mrt_tiles_packed_floats(width, height, rank, count, ctypes.byref(n)), "mrt_tiles_packed_floats")
+    return n.value
+
+
+def tiles_pack(image_ptr: int, width: int, height: int, rank: int, count: int, packed_ptr: int, stream=None,
+               sync=True) -> None:
+    """A shard's owned tiles of a device image -> dense [tile][64*64] RGBA32F (multi-GPU exchange)."""
+    _check(lib().mrt_tiles_pack(image_ptr, width, height, rank, count, packed_ptr, stream), "mrt_tiles_pack")
+    if sync:
+        synchronize(stream)
+
+
+def tiles_unpack(packed_ptr: int, width: int, height: int, rank: int, count: int, image_ptr: int, stream=None,
+                 sync=True) -> None:
+    _check(lib().mrt_tiles_unpack(packed_ptr, width, height, rank, count, image_ptr, stream), "mrt_tiles_unpack")
+    if sync:
+        synchronize(stream)
+
+
+def tiles_pack_host(image, rank: int, count: int):
+    """numpy restatement of mrt_tiles_pack (host rehearsal of the exchange; image is H x W x 4)."""
+    import numpy as np
+    H, W = image.shape[:2]
+    tx_n, ty_n = (W + 63) // 64, (H + 63) // 64
+    tiles = list(range(rank, tx_n * ty_n, count))
+    out = np.zeros((len(tiles), 64, 64, 4), np.float32)
+    for k, t in enumerate(tiles):
+        ty, tx = divmod(t, tx_n)
+        blk = image[ty * 64:(ty + 1) * 64, tx * 64:(tx + 1) * 64]
+        out[k, :blk.shape[0], :blk.shape[1]] = blk
+    return out
+
+
+def tiles_unpack_host(packed, image, rank: int, count: int) -> None:
+    H, W = image.shape[:2]
+    tx_n, ty_n = (W + 63) // 64, (H + 63) // 64
+    for k, t in enumerate(range(rank, tx_n * ty_n, count)):
+        ty, tx = divmod(t, tx_n)
+        h, w = min(64, H - ty * 64), min(64, W - tx * 64)
+        image[ty * 64:ty * 64 + h, tx * 64:tx * 64 + w] = packed[k, :h, :w]
 
 
 def debug_stamps(reset: bool = True):

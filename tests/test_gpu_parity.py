@@ -192,7 +192,7 @@ def test_frame_batching_invariance(gpu, mrt_mod, monkeypatch, scene):
     sc = _scene(mrt_mod, scene)
     W, H, L = 136, 72, 5
     out = {}
-    for batch, draws in [(1, (7,)), (3, (7,)), (8, (7,)), (3, (4, 3)), (2, (1, 5, 1))]:
+    for batch, draws in [(1, (7,)), (3, (7,)), (8, (7,)), (64, (7,)), (3, (4, 3)), (2, (1, 5, 1))]:
         monkeypatch.setenv("MRT_BATCH", str(batch))
         r = mrt_mod.Renderer(sc, W, H, L, shard_rank=1, shard_count=2)
         for d in draws:
@@ -238,3 +238,21 @@ def test_save_image_roundtrip(gpu, mrt_mod, tmp_path):
         header = f.readline() + f.readline() + f.readline()
         data = np.frombuffer(f.read(), "<f4").reshape(48, 64, 3)
     assert header.startswith(b"PF") and np.array_equal(data, img[..., :3])
+
+
+@pytest.mark.parametrize("W,H,count", [(200, 150, 3), (1920, 1080, 8), (64, 64, 1)])
+def test_tiles_pack_unpack(gpu, mrt_mod, W, H, count):
+    """Device tile pack (multi-GPU exchange) == its numpy restatement; unpacking
+    every shard's packed tiles rebuilds the image bitwise."""
+    rng = np.random.default_rng(W + count)
+    img = rng.standard_normal((H, W, 4)).astype(np.float32)
+    d_img = to_dev(img)
+    d_out = to_dev(np.zeros_like(img))
+    for k in range(count):
+        n = mrt_mod.tiles_packed_floats(W, H, k, count)
+        d_p = to_dev(np.zeros(n, np.float32))
+        mrt_mod.tiles_pack(dev_ptr(d_img), W, H, k, count, dev_ptr(d_p))
+        got = from_dev(d_p, np.float32)
+        assert got.tobytes() == mrt_mod.tiles_pack_host(img, k, count).tobytes()
+        mrt_mod.tiles_unpack(dev_ptr(d_p), W, H, k, count, dev_ptr(d_out))
+    assert from_dev(d_out, np.float32).tobytes() == img.tobytes()
