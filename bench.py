@@ -54,8 +54,8 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--precise", action="store_true", help="time the parity build instead of the fast build")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--bvh", default="sah", choices=["sah", "lbvh"],
-                   help="BVH builder: host binned SAH (default) or the device LBVH (MRT_BVH_DEVICE_LBVH)")
+    p.add_argument("--bvh", default="sah", choices=["sah", "lbvh", "ploc"],
+                   help="BVH builder: host binned SAH (default), device LBVH or device PLOC")
     p.add_argument("--cpu-frames", type=int, default=0,
                    help="frames of the workload timed on the CPU oracle (default: all spp frames for C2, 8 otherwise)")
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
@@ -148,7 +148,8 @@ def main():
             dist.init_process_group("gloo")
     W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
     scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=device,
-                      bvh_builder=mrt.BVH_DEVICE_LBVH if args.bvh == "lbvh" else mrt.BVH_HOST_SAH)
+                      bvh_builder={"sah": mrt.BVH_HOST_SAH, "lbvh": mrt.BVH_DEVICE_LBVH,
+                                   "ploc": mrt.BVH_DEVICE_PLOC}[args.bvh])
     # the accumulation image lives in a torch tensor so RCCL can reduce it in
     # place; libmrt renders into it on its own stream (torch ships its own HIP
     # runtime copy, so streams are not shared: r.sync() orders the reduce)
@@ -269,7 +270,7 @@ def main():
                    "scene": cfg["scene"], "parallelism": (f"tile shard 0 of {shard_count} (one GPU's share)" if args.shard_of else
                                    f"tiles64x{world}" + (f" + rccl {args.exchange}" if world > 1 else "")),
                    "build": "precise" if args.precise else "fast",
-                   "bvh": {"builder": "device-lbvh" if args.bvh == "lbvh" else "host-sah",
+                   "bvh": {"builder": {"sah": "host-sah", "lbvh": "device-lbvh", "ploc": "device-ploc"}[args.bvh],
                            "build_ms": round(scene.info["build_ms"], 2), "nodes": scene.info["bvh_nodes"],
                            "max_stack": scene.info["bvh_max_stack"]}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -79,7 +79,9 @@ typedef struct mrt_scene_desc {
 /* BVH builders */
 #define MRT_BVH_HOST_SAH 1u      /* host binned-SAH BVH2, collapsed to BVH4 (best traversal quality) */
 #define MRT_BVH_DEVICE_LBVH 2u   /* device linear BVH (Morton sort + radix tree, collapsed to BVH4
-                                    on the GPU; BVH4 only) — builds from device buffers, no host copy */
+                                    on the GPU; BVH4 only) — fastest build, weakest tree */
+#define MRT_BVH_DEVICE_PLOC 3u   /* device PLOC (Morton sort + nearest-neighbour clustering, collapsed
+                                    to BVH4 on the GPU) — near-SAH tree; builds from device buffers */
 
 typedef struct mrt_scene_info {
   uint32_t vertices, triangles, materials, light_triangles;
@@ -116,7 +118,7 @@ typedef struct mrt_accel_desc {
   const uint32_t* indices;         /* device pointer: 3 uint32 per triangle */
   uint32_t triangle_count;
   int device;                      /* HIP device of the buffers */
-  uint32_t builder;                /* MRT_BVH_*; 0 = default (MRT_BVH_DEVICE_LBVH) */
+  uint32_t builder;                /* MRT_BVH_*; 0 = default (MRT_BVH_DEVICE_PLOC) */
   uint32_t max_leaf_size;          /* 0 = default (4) */
   void* stream;                    /* hipStream_t of libmrt's runtime, NULL = own stream */
 } mrt_accel_desc;

@@ -91,8 +91,9 @@ struct AccumArgs {
 #define MRT_DECLARE_LAUNCHERS(NS)                                                                         \
   namespace NS {                                                                                          \
   hipError_t launch_raygen(uint32_t W, uint32_t H, const float* noise, RefRay* rays, hipStream_t s);      \
+  /* spill: >= (max_stack - 32) * kIntersectSpillGrid * 256 uint32 when sc.max_stack > kMaxStack */       \
   hipError_t launch_intersect(const DeviceScene& sc, const void* rays, uint32_t stride, uint32_t count,   \
-                              RefIntersection* out, hipStream_t s);                                       \
+                              RefIntersection* out, uint32_t* spill, hipStream_t s);                      \
   hipError_t launch_shade(const DeviceScene& sc, uint32_t W, uint32_t H, uint32_t frame_index,            \
                           uint32_t max_path_length, const float* noise, const RefIntersection* isect,     \
                           RefRay* rays, RefShadowRay* srays, hipStream_t s);                              \

@@ -1103,26 +1103,26 @@ __global__ __launch_bounds__(kBlock) void raygen_kernel(uint32_t W, uint32_t H, 
   for (int k = 0; k < 3; ++k) { r.throughput[k] = 1.0f; r.radiance[k] = 0.0f; }
 }
 
-template <int WIDTH>
+template <int WIDTH, int STACK>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DeviceScene sc, const uint8_t* rays, uint32_t stride,
-                                                           uint32_t count, RefIntersection* out) {
-  const LdsCtx cx = stage_lds<kGlobal>(sc, 0);
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= count) return;
-  const float* r = reinterpret_cast<const float*>(rays + (size_t)i * stride);
-  RefIntersection res{-1.0f, 0xFFFFFFFFu, {0.0f, 0.0f}};
-  const float tmax = r[7];
-  if (tmax >= 0.0f) {   // maxDistance < 0 disables the ray (Shaders.metal:124,173)
-    const V3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
-    const Hit h = trace_nearest<kMaxStack, kGlobal, WIDTH>(sc, cx, o, d, r[3], tmax);
-    if (h.found) {
-      res.distance = h.t;
-      res.triangleIndex = h.prim;
-      res.coordinates[0] = h.u;
-      res.coordinates[1] = h.v;
+                                                           uint32_t count, RefIntersection* out, uint32_t* spill) {
+  const LdsCtx cx = stage_lds<kGlobal>(sc, 0, spill);
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < count; i += gridDim.x * kBlock) {
+    const float* r = reinterpret_cast<const float*>(rays + (size_t)i * stride);
+    RefIntersection res{-1.0f, 0xFFFFFFFFu, {0.0f, 0.0f}};
+    const float tmax = r[7];
+    if (tmax >= 0.0f) {   // maxDistance < 0 disables the ray (Shaders.metal:124,173)
+      const V3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
+      const Hit h = trace_nearest<STACK, kGlobal, WIDTH>(sc, cx, o, d, r[3], tmax);
+      if (h.found) {
+        res.distance = h.t;
+        res.triangleIndex = h.prim;
+        res.coordinates[0] = h.u;
+        res.coordinates[1] = h.v;
+      }
     }
+    out[i] = res;
   }
-  out[i] = res;
 }
 
 __global__ __launch_bounds__(kBlock) void shade_kernel(DeviceScene sc, uint32_t W, uint32_t H, uint32_t f,
@@ -1296,15 +1296,20 @@ hipError_t launch_raygen(uint32_t W, uint32_t H, const float* noise, RefRay* ray
 }
 
 hipError_t launch_intersect(const DeviceScene& sc, const void* rays, uint32_t stride, uint32_t count,
-                            RefIntersection* out, hipStream_t s) {
+                            RefIntersection* out, uint32_t* spill, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  const size_t lds = (size_t)kMaxStack * kBlock * 4;
-  if (sc.width == 4)
-    intersect_kernel<4><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, reinterpret_cast<const uint8_t*>(rays),
-                                                                           stride, count, out);
-  else
-    intersect_kernel<2><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, reinterpret_cast<const uint8_t*>(rays),
-                                                                           stride, count, out);
+  const uint8_t* r = reinterpret_cast<const uint8_t*>(rays);
+  if (sc.max_stack <= (uint32_t)kMaxStack) {   // whole stack in LDS
+    const size_t lds = (size_t)kMaxStack * kBlock * 4;
+    if (sc.width == 4) intersect_kernel<4, kMaxStack><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);
+    else intersect_kernel<2, kMaxStack><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);
+  } else {                                      // 32 LDS entries + global spill, persistent grid
+    if (!spill) return hipErrorInvalidValue;
+    const size_t lds = (size_t)32 * kBlock * 4;
+    const dim3 g(std::min<uint32_t>(blocks_for(count), kIntersectSpillGrid));
+    if (sc.width == 4) intersect_kernel<4, -32><<<g, dim3(kBlock), lds, s>>>(sc, r, stride, count, out, spill);
+    else intersect_kernel<2, -32><<<g, dim3(kBlock), lds, s>>>(sc, r, stride, count, out, spill);
+  }
   return hipGetLastError();
 }
 

@@ -77,7 +77,9 @@ constexpr int32_t kEmptyChild = 0x7FFFFFFF;
 constexpr int kLeafCountBits = 4;
 constexpr int kMaxLeafSize = 1 << kLeafCountBits;   // 16
 constexpr int kMaxBvhDepth = 32;                    // builder forces leaves below this binary depth
-constexpr int kMaxStack = 64;                       // traversal stack entries per ray (host SAH BVH4 < 1.5 x depth; device LBVH deeper)
+constexpr int kMaxStack = 64;                       // LDS traversal stack of the stage intersect kernel (host SAH BVH4 < 1.5 x depth)
+constexpr int kMaxTraversalStack = 256;             // deepest supported tree (stack entries beyond LDS spill to global memory)
+constexpr uint32_t kIntersectSpillGrid = 1024;      // persistent grid of the stage intersect kernel's spill variant
 
 // Device-resident scene, passed to kernels by value.  Every pointer is
 // 16-B aligned device memory; float pointers documented as "float4" hold
@@ -99,7 +101,7 @@ struct DeviceScene {
   uint32_t num_lights;       // light triangles, excluding the sentinel (SharedData.lightTrianglesCount)
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
   uint32_t width;            // 2 = BVH2, 4 = BVH4
-  uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxStack)
+  uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack)
 };
 
 }  // namespace mrt

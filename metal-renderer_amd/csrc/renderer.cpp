@@ -59,6 +59,13 @@ struct DevBuf {
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// traversal-stack spill of the stage intersect kernel (trees deeper than its
+// kMaxStack-entry LDS stack): (need - 32) entries x its persistent grid
+hipError_t alloc_isect_spill(DevBuf& b, uint32_t max_stack) {
+  if (max_stack <= (uint32_t)mrt::kMaxStack) return b.alloc(0);
+  return b.alloc((size_t)(max_stack - 32) * mrt::kIntersectSpillGrid * 256 * 4);
+}
+
 hipError_t upload(DevBuf& b, const void* src, size_t n) {
   hipError_t e = b.alloc(std::max<size_t>(n, 16));
   if (e != hipSuccess) return e;
@@ -71,12 +78,14 @@ hipError_t upload(DevBuf& b, const void* src, size_t n) {
 struct mrt_accel {
   mrt_accel_desc desc{};
   DevBuf nodes, tris;
+  DevBuf isect_spill;       // stage intersect stack spill for trees deeper than kMaxStack
   mrt::DeviceScene dev{};
   mrt_accel_info info{};
 };
 
 struct mrt_scene {
   int device = 0;
+  DevBuf isect_spill;       // stage intersect stack spill for trees deeper than kMaxStack
   mrt::HostScene host;
   mrt::BvhResult bvh;
   DevBuf nodes, tris, prims, materials, lights;
@@ -428,9 +437,10 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
   if (opt.width != 2 && opt.width != 4) return fail(MRT_ERR_INVALID, "bvh_width must be 2 or 4");
   const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
-  if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH) return fail(MRT_ERR_INVALID, "unknown bvh_builder");
-  if (builder == MRT_BVH_DEVICE_LBVH && desc->device < 0) return fail(MRT_ERR_INVALID, "device BVH build needs a device");
-  if (builder == MRT_BVH_DEVICE_LBVH && opt.width != 4) return fail(MRT_ERR_INVALID, "device BVH build is BVH4 only");
+  if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH && builder != MRT_BVH_DEVICE_PLOC)
+    return fail(MRT_ERR_INVALID, "unknown bvh_builder");
+  if (builder != MRT_BVH_HOST_SAH && desc->device < 0) return fail(MRT_ERR_INVALID, "device BVH build needs a device");
+  if (builder != MRT_BVH_HOST_SAH && opt.width != 4) return fail(MRT_ERR_INVALID, "device BVH build is BVH4 only");
   double build_ms = 0.0;
   if (builder == MRT_BVH_HOST_SAH) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -445,7 +455,8 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     HIP_TRY(upload(dv, h.vertices.data(), h.vertices.size() * sizeof(mrt::RefVertex)));
     HIP_TRY(upload(di, h.indices.data(), h.indices.size() * 4));
     mrt::GpuBvhResult g;
-    if (mrt::build_bvh_gpu(dv.as<float>(), sizeof(mrt::RefVertex), di.as<uint32_t>(), T, opt.max_leaf_size, nullptr, g,
+    if (mrt::build_bvh_gpu(dv.as<float>(), sizeof(mrt::RefVertex), di.as<uint32_t>(), T, opt.max_leaf_size,
+                           builder == MRT_BVH_DEVICE_PLOC ? mrt::GpuBvhAlgo::kPloc : mrt::GpuBvhAlgo::kLbvh, nullptr, g,
                            err) != hipSuccess)
       return fail(MRT_ERR_HIP, "device BVH build failed: " + err);
     s->nodes.p = g.nodes; s->nodes.bytes = g.nodes_bytes;
@@ -467,7 +478,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     b.lds_nodes = std::min<uint32_t>(opt.lds_node_budget, g.num_nodes);   // BFS order: any prefix is the top
     b.sah_cost = 0.0;
   }
-  if (s->bvh.max_stack > (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack");
+  if (s->bvh.max_stack > (uint32_t)mrt::kMaxTraversalStack)
+    return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack (" + std::to_string(s->bvh.max_stack) + " entries, " +
+                                     std::to_string(s->bvh.wide_depth) + " levels)");
 
   // per-primitive shading records (primitive order)
   std::vector<float> prims((size_t)T * 24);
@@ -541,6 +554,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.lds_nodes = s->bvh.lds_nodes;
   d.width = s->bvh.width;
   d.max_stack = s->bvh.max_stack;
+  HIP_TRY(alloc_isect_spill(s->isect_spill, d.max_stack));
   in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
   *out = s.release();
   return MRT_OK;
@@ -581,7 +595,7 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
   while (!stack.empty()) {
     Item it = stack.back();
     stack.pop_back();
-    if (it.depth >= (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_STATE, "BVH too deep");
+    if (it.depth >= (uint32_t)mrt::kMaxTraversalStack) return fail(MRT_ERR_STATE, "BVH too deep");
     if (it.ref >= 0) {
       if ((uint32_t)it.ref >= b.num_nodes) return fail(MRT_ERR_STATE, "BVH node index out of range");
       ++nodes_seen;
@@ -655,10 +669,11 @@ int accel_build(mrt_accel* a) {
   HIP_TRY(hipSetDevice(d.device));
   hipStream_t s = (hipStream_t)d.stream;
   std::string err;
-  if (a->info.builder == MRT_BVH_DEVICE_LBVH) {
+  if (a->info.builder != MRT_BVH_HOST_SAH) {
     mrt::GpuBvhResult g;
-    if (mrt::build_bvh_gpu(reinterpret_cast<const float*>(d.vertices), d.vertex_stride, d.indices, T, leaf, s, g,
-                           err) != hipSuccess)
+    if (mrt::build_bvh_gpu(reinterpret_cast<const float*>(d.vertices), d.vertex_stride, d.indices, T, leaf,
+                           a->info.builder == MRT_BVH_DEVICE_PLOC ? mrt::GpuBvhAlgo::kPloc : mrt::GpuBvhAlgo::kLbvh,
+                           s, g, err) != hipSuccess)
       return fail(MRT_ERR_HIP, "device BVH build failed: " + err);
     (void)a->nodes.alloc(0);
     (void)a->tris.alloc(0);
@@ -703,7 +718,8 @@ int accel_build(mrt_accel* a) {
     a->info.bvh_levels = b.wide_depth;
     a->info.bvh_max_stack = b.max_stack;
   }
-  if (a->dev.max_stack > (uint32_t)mrt::kMaxStack) return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack");
+  if (a->dev.max_stack > (uint32_t)mrt::kMaxTraversalStack) return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack");
+  HIP_TRY(alloc_isect_spill(a->isect_spill, a->dev.max_stack));
   a->dev.nodes = a->nodes.as<float>();
   a->dev.tris = a->tris.as<float>();
   a->dev.num_triangles = T;
@@ -722,8 +738,9 @@ int mrt_accel_create(const mrt_accel_desc* desc, mrt_accel** out) {
     return fail(MRT_ERR_INVALID, "mrt_accel_create: null buffer");
   if (desc->vertex_stride < 12 || desc->vertex_stride % 4) return fail(MRT_ERR_INVALID, "mrt_accel_create: bad vertex_stride");
   if (desc->max_leaf_size > (uint32_t)mrt::kMaxLeafSize) return fail(MRT_ERR_INVALID, "mrt_accel_create: max_leaf_size > 16");
-  const uint32_t builder = desc->builder ? desc->builder : MRT_BVH_DEVICE_LBVH;
-  if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH) return fail(MRT_ERR_INVALID, "unknown builder");
+  const uint32_t builder = desc->builder ? desc->builder : MRT_BVH_DEVICE_PLOC;
+  if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH && builder != MRT_BVH_DEVICE_PLOC)
+    return fail(MRT_ERR_INVALID, "unknown builder");
   std::unique_ptr<mrt_accel> a(new mrt_accel());
   a->desc = *desc;
   a->info.builder = builder;
@@ -744,9 +761,11 @@ int mrt_accel_intersect(const mrt_accel* accel, const void* rays, uint32_t strid
     return fail(MRT_ERR_INVALID, "mrt_accel_intersect: bad argument");
   HIP_TRY(hipSetDevice(accel->desc.device));
   if (precise(flags))
-    HIP_TRY(mrt::precise::launch_intersect(accel->dev, rays, stride, count, (mrt::RefIntersection*)isect, (hipStream_t)stream));
+    HIP_TRY(mrt::precise::launch_intersect(accel->dev, rays, stride, count, (mrt::RefIntersection*)isect,
+                                           accel->isect_spill.as<uint32_t>(), (hipStream_t)stream));
   else
-    HIP_TRY(mrt::fast::launch_intersect(accel->dev, rays, stride, count, (mrt::RefIntersection*)isect, (hipStream_t)stream));
+    HIP_TRY(mrt::fast::launch_intersect(accel->dev, rays, stride, count, (mrt::RefIntersection*)isect,
+                                        accel->isect_spill.as<uint32_t>(), (hipStream_t)stream));
   return MRT_OK;
 }
 
@@ -778,7 +797,8 @@ int mrt_intersect(const mrt_scene* scene, const void* rays, uint32_t stride, uin
                   uint32_t flags, void* stream) {
   if (!scene || (!rays && count) || (!isect && count) || stride < 32 || (stride % 4))
     return fail(MRT_ERR_INVALID, "mrt_intersect: bad argument");
-  STAGE_CALL(launch_intersect(scene->dev, rays, stride, count, (mrt::RefIntersection*)isect, (hipStream_t)stream));
+  STAGE_CALL(launch_intersect(scene->dev, rays, stride, count, (mrt::RefIntersection*)isect,
+                              scene->isect_spill.as<uint32_t>(), (hipStream_t)stream));
   return MRT_OK;
 }
 

@@ -58,7 +58,7 @@ class SceneDesc(ctypes.Structure):
     ]
 
 
-BVH_HOST_SAH, BVH_DEVICE_LBVH = 1, 2
+BVH_HOST_SAH, BVH_DEVICE_LBVH, BVH_DEVICE_PLOC = 1, 2, 3
 
 
 class AccelDesc(ctypes.Structure):

@@ -1,4 +1,4 @@
-"""GPU: the device BVH builder (LBVH, MRT_BVH_DEVICE_LBVH) and the MPS-shaped
+"""GPU: the device BVH builders (LBVH and PLOC) and the MPS-shaped
 acceleration-structure ABI over raw device buffers (mrt_accel_*), the
 replacement for MPSTriangleAccelerationStructure + MPSRayIntersector
 (renderer/Renderer.mm:456-469).
@@ -33,21 +33,26 @@ def _isect_bits(a):
     return a.view(np.uint32).reshape(-1, 4)
 
 
+DEVICE_BUILDERS = [2, 3]   # MRT_BVH_DEVICE_LBVH, MRT_BVH_DEVICE_PLOC
+
+
 @pytest.mark.parametrize("scene,proc", [("cornellbox", 0), ("CornellBox-Water-plastic", 0), ("cornellbox", 65536)])
 @pytest.mark.parametrize("leaf", [1, 4])
-def test_device_lbvh_structure(gpu, mrt_mod, scene, proc, leaf):
-    s = mrt_mod.Scene(scene, procedural_triangles=proc, max_leaf_size=leaf, bvh_builder=mrt_mod.BVH_DEVICE_LBVH)
+@pytest.mark.parametrize("builder", DEVICE_BUILDERS)
+def test_device_bvh_structure(gpu, mrt_mod, scene, proc, leaf, builder):
+    s = mrt_mod.Scene(scene, procedural_triangles=proc, max_leaf_size=leaf, bvh_builder=builder)
     s.check_bvh()   # every primitive in exactly one leaf, boxes contain triangles, stack bound
     i = s.info
     assert i["bvh_width"] == 4 and i["triangles"] >= proc
-    assert 0 < i["bvh_nodes"] <= i["triangles"] and i["bvh_max_stack"] <= 64
+    assert 0 < i["bvh_nodes"] <= i["triangles"] and i["bvh_max_stack"] <= 256
     assert i["bvh_lds_nodes"] <= i["bvh_nodes"] and i["build_ms"] > 0
     s.close()
 
 
 @pytest.mark.parametrize("scene", ["cornellbox", "white-box", "CornellBox-Water-plastic"])
-def test_device_lbvh_intersect_bitexact(gpu, mrt_mod, oracle_mod, scene):
-    s = mrt_mod.Scene(scene, bvh_builder=mrt_mod.BVH_DEVICE_LBVH)
+@pytest.mark.parametrize("builder", DEVICE_BUILDERS)
+def test_device_bvh_intersect_bitexact(gpu, mrt_mod, oracle_mod, scene, builder):
+    s = mrt_mod.Scene(scene, bvh_builder=builder)
     osc = oracle_mod.OracleScene(mrt_mod.scene_path(scene))
     rays = np.concatenate([_rays(oracle_mod, 6000, np.random.default_rng(11)),
                            oracle_mod.raygen(80, 60, oracle_mod.noise_table(SEED, 0))]).astype(oracle_mod.RAY_DTYPE)
@@ -61,19 +66,20 @@ def test_device_lbvh_intersect_bitexact(gpu, mrt_mod, oracle_mod, scene):
 
 
 @pytest.mark.parametrize("scene,L", [("cornellbox", 4), ("CornellBox-Water-plastic", 8)])
-def test_render_lbvh_equals_sah(gpu, mrt_mod, oracle_mod, scene, L):
+def test_render_device_bvh_equals_sah(gpu, mrt_mod, oracle_mod, scene, L):
     """The image does not depend on the BVH: precise renders over the device
-    LBVH and the host SAH BVH are bit-identical, and match the oracle."""
+    LBVH / PLOC trees and the host SAH BVH are bit-identical, and match the oracle."""
     W, H, frames = 96, 64, 3
     imgs = []
-    for builder in (mrt_mod.BVH_HOST_SAH, mrt_mod.BVH_DEVICE_LBVH):
+    for builder in (mrt_mod.BVH_HOST_SAH, mrt_mod.BVH_DEVICE_LBVH, mrt_mod.BVH_DEVICE_PLOC):
         s = mrt_mod.Scene(scene, bvh_builder=builder)
         r = mrt_mod.Renderer(s, W, H, L, precise=True)
         r.draw(frames)
         imgs.append((r.read_image(), r.stats()["active_ray_bounces"]))
         r.close()
         s.close()
-    assert imgs[0][0].tobytes() == imgs[1][0].tobytes() and imgs[0][1] == imgs[1][1]
+    for img, a in imgs[1:]:
+        assert img.tobytes() == imgs[0][0].tobytes() and a == imgs[0][1]
     ref, A = oracle_mod.OracleScene(mrt_mod.scene_path(scene)).render(W, H, L, SEED, frames, threads=8)
     rel, rmse, _ = pixel_metrics(imgs[1][0], ref)
     assert np.mean(rel <= 1e-4) >= 0.999 and rmse <= 1e-3
@@ -86,7 +92,7 @@ def _export_dev(mrt_mod, scene, proc=0):
     return e
 
 
-@pytest.mark.parametrize("builder", [1, 2])
+@pytest.mark.parametrize("builder", [1, 2, 3])
 def test_accel_raw_buffers_bitexact(gpu, mrt_mod, oracle_mod, builder):
     """mrt_accel_* over the reference's own Vertex (24 B) / uint32 index buffers."""
     scene = "CornellBox-Water-plastic"
@@ -119,7 +125,8 @@ def test_accel_rebuild_after_vertex_update(gpu, mrt_mod, oracle_mod):
     e = _export_dev(mrt_mod, "cornellbox", proc=20000)
     T = len(e["indices"]) // 3
     d_v, d_i = to_dev(e["vertices"]), to_dev(e["indices"])
-    lb = mrt_mod.Accel(dev_ptr(d_v), 24, dev_ptr(d_i), T, builder=mrt_mod.BVH_DEVICE_LBVH)
+    lb = mrt_mod.Accel(dev_ptr(d_v), 24, dev_ptr(d_i), T)   # default builder: device PLOC
+    assert lb.info()["builder"] == mrt_mod.BVH_DEVICE_PLOC
     v2 = e["vertices"].copy()
     v2["v"] = v2["v"] * np.float32(0.9) + np.float32(0.05)
     d_v.copy_(to_dev(v2))
@@ -149,14 +156,46 @@ def test_accel_tiny_and_empty(gpu, mrt_mod, oracle_mod, T):
     rays = _rays(oracle_mod, 4000, np.random.default_rng(T))
     d_rays = to_dev(rays)
     outs = []
-    for builder in ([mrt_mod.BVH_DEVICE_LBVH] + ([mrt_mod.BVH_HOST_SAH] if T else [])):
+    for builder in ([mrt_mod.BVH_DEVICE_PLOC, mrt_mod.BVH_DEVICE_LBVH] + ([mrt_mod.BVH_HOST_SAH] if T else [])):
         acc = mrt_mod.Accel(dev_ptr(d_v), 24, dev_ptr(d_i), T, builder=builder)
         d_out = to_dev(np.zeros(len(rays), oracle_mod.ISECT_DTYPE))
         acc.intersect(dev_ptr(d_rays), 80, len(rays), dev_ptr(d_out), precise=True)
         outs.append(from_dev(d_out, oracle_mod.ISECT_DTYPE))
         acc.close()
     if T == 0:
-        assert (outs[0]["distance"] == -1.0).all() and (outs[0]["triangleIndex"] == 0xFFFFFFFF).all()
+        for o in outs:
+            assert (o["distance"] == -1.0).all() and (o["triangleIndex"] == 0xFFFFFFFF).all()
     else:
         assert (outs[0]["distance"] >= 0).any()
-        assert (_isect_bits(outs[0]) == _isect_bits(outs[1])).all()
+        for o in outs[1:]:
+            assert (_isect_bits(o) == _isect_bits(outs[0])).all()
+
+
+@pytest.mark.parametrize("builder", DEVICE_BUILDERS)
+def test_device_bvh_deep_scene_matches_sah(gpu, mrt_mod, oracle_mod, builder):
+    """1M-triangle procedural scene (BASELINE C4): the device trees are deeper
+    than the stage kernel's LDS stack (spill variant), and still answer every
+    ray bitwise like the host-SAH tree; a short render agrees bitwise too."""
+    proc = 1 << 20
+    scenes = [mrt_mod.Scene("cornellbox", procedural_triangles=proc, bvh_builder=b)
+              for b in (mrt_mod.BVH_HOST_SAH, builder)]
+    scenes[1].check_bvh()
+    rays = _rays(oracle_mod, 50000, np.random.default_rng(17))
+    d_rays = to_dev(rays)
+    outs = []
+    for sc in scenes:
+        d_out = to_dev(np.zeros(len(rays), oracle_mod.ISECT_DTYPE))
+        mrt_mod.intersect(sc, dev_ptr(d_rays), 80, len(rays), dev_ptr(d_out), precise=True)
+        outs.append(from_dev(d_out, oracle_mod.ISECT_DTYPE))
+    assert (outs[0]["distance"] >= 0).mean() > 0.5
+    assert (_isect_bits(outs[0]) == _isect_bits(outs[1])).all()
+    imgs = []
+    for sc in scenes:
+        r = mrt_mod.Renderer(sc, 128, 96, 4, precise=True)
+        r.draw(2)
+        imgs.append(r.read_image())
+        r.close()
+    assert imgs[0].tobytes() == imgs[1].tobytes()
+    print(f"builder {builder}: max_stack {scenes[1].info['bvh_max_stack']}, build {scenes[1].info['build_ms']:.1f} ms")
+    for sc in scenes:
+        sc.close()
