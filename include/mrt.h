@@ -202,6 +202,9 @@ int mrt_renderer_sync(mrt_renderer* r);
 int mrt_renderer_image(mrt_renderer* r, float** device_image);
 /* Synchronise and copy the image to host memory (rgba must hold W*H*4 floats). */
 int mrt_renderer_read_image(mrt_renderer* r, float* rgba, size_t count);
+/* MAX_FRAMES (Raytracing.h:28, Renderer.mm:589-590): once frame_index reaches
+ * max_frames, draws are no-ops (0 = unlimited, the reference's default). */
+int mrt_renderer_set_max_frames(mrt_renderer* r, uint32_t max_frames);
 /* Save the image top-down as .pfm (float RGB) or .exr (float RGBA, uncompressed). */
 int mrt_renderer_save_image(mrt_renderer* r, const char* path);
 int mrt_renderer_stats(const mrt_renderer* r, mrt_stats* stats);
@@ -218,6 +221,18 @@ int mrt_noise_table(uint64_t seed, int64_t frame, float* out16384);
  * (row 0 = bottom); returns the number of owned pixels via *owned. */
 int mrt_shard_mask(uint32_t width, uint32_t height, uint32_t shard_rank, uint32_t shard_count, uint8_t* mask,
                    uint64_t* owned);
+/* Display (blitFragment, Shaders.metal:33-70): the reference's compile-time
+ * blit switches as flags — tone map 1 - exp(-c) (ENABLE_TONE_MAPPING),
+ * toSRGB (MANUAL_SRGB, Raytracing.h:130-135), and COMPARISON_MODE 1..4
+ * against a reference image (e.g. a Mitsuba golden, Renderer.mm:162-253)
+ * scaled by compare_scale (COMPARISON_SCALE = 10).  Device pointers, W*H
+ * RGBA32F in and out; `reference` may be NULL when no compare mode is set. */
+#define MRT_DISPLAY_TONEMAP 1u
+#define MRT_DISPLAY_SRGB 2u
+#define MRT_DISPLAY_COMPARE(mode) ((uint32_t)(mode) << 8)   /* 1 abs, 2 ref-to-color, 3 color-to-ref, 4 luminance */
+int mrt_display(const float* image, const float* reference, float* out, uint32_t width, uint32_t height,
+                uint32_t flags, float compare_scale, void* stream);
+
 /* Multi-GPU exchange of the accumulation image: a shard's
  * owned 64x64 tiles packed densely, [k][64*64] RGBA32F for its k-th owned
  * tile (tile t = shard_rank + k*shard_count, row-major tiles; zeros outside

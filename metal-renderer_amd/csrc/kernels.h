@@ -110,6 +110,9 @@ struct AccumArgs {
                            uint32_t grid, hipStream_t s);                                                 \
   /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \
   hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s);                                  \
+  /* blitFragment (Shaders.metal:33-70): tone map / sRGB / golden comparison of the RGBA32F image */     \
+  hipError_t launch_display(const float4* image, const float4* reference, float4* out, uint32_t n,        \
+                            uint32_t flags, float compare_scale, hipStream_t s);                          \
   /* owned-tile exchange: pack a shard's tiles of a W x H RGBA32F image into                             \
      [owned tile][64 x 64] float4 (zeros outside the image), or unpack them back (bitwise moves) */     \
   hipError_t launch_tiles_move(const float4* src, float4* dst, uint32_t W, uint32_t H, uint32_t rank,    \

@@ -1341,6 +1341,62 @@ hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// blitFragment — renderer/Shaders.metal:33-70 with the compile-time switches
+// of Raytracing.h:11-12,25-31 as runtime flags (include/mrt.h MRT_DISPLAY_*):
+// tone map 1 - exp(-c) (ENABLE_TONE_MAPPING), toSRGB on rgb (MANUAL_SRGB,
+// Raytracing.h:130-135), then the COMPARISON_MODE against a reference image
+// scaled by COMPARISON_SCALE.  One output pixel per image pixel (the
+// reference samples the W x H texture with a nearest filter).
+__device__ __forceinline__ float to_srgb(float v) {   // Raytracing.h:130-135
+  if (v <= 0.0f) return 0.0f;
+  if (v >= 1.0f) return 1.0f;
+#if MRT_PRECISE
+  return (v < 0.0031308f) ? (12.92f * v) : (1.055f * powf(v, 1.0f / 2.4f) - 0.055f);
+#else
+  return (v < 0.0031308f) ? (12.92f * v) : (1.055f * __powf(v, 1.0f / 2.4f) - 0.055f);
+#endif
+}
+__device__ __forceinline__ float4 display_map(float4 c, uint32_t flags) {
+  if (flags & 1u) {   // tone mapping (applies to all four channels, as color = 1 - exp(-color))
+#if MRT_PRECISE
+    c = make_float4(1.0f - expf(-c.x), 1.0f - expf(-c.y), 1.0f - expf(-c.z), 1.0f - expf(-c.w));
+#else
+    c = make_float4(1.0f - __expf(-c.x), 1.0f - __expf(-c.y), 1.0f - __expf(-c.z), 1.0f - __expf(-c.w));
+#endif
+  }
+  if (flags & 2u) c = make_float4(to_srgb(c.x), to_srgb(c.y), to_srgb(c.z), c.w);
+  return c;
+}
+__global__ __launch_bounds__(kBlock) void display_kernel(const float4* image, const float4* reference, float4* out,
+                                                         uint32_t n, uint32_t flags, float scale) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float4 c = display_map(image[i], flags);
+  const uint32_t mode = (flags >> 8) & 0xFFu;
+  if (mode == 0u || !reference) { out[i] = c; return; }
+  const float4 r = display_map(reference[i], flags);   // the reference texture goes through the same blit
+  float4 o;
+  if (mode == 1u) {          // COMPARE_ABSOLUTE_VALUE
+    o = make_float4(fabsf(c.x - r.x), fabsf(c.y - r.y), fabsf(c.z - r.z), fabsf(c.w - r.w));
+  } else if (mode == 2u) {   // COMPARE_REF_TO_COLOR
+    o = make_float4(fmaxf(0.0f, r.x - c.x), fmaxf(0.0f, r.y - c.y), fmaxf(0.0f, r.z - c.z), fmaxf(0.0f, r.w - c.w));
+  } else if (mode == 3u) {   // COMPARE_COLOR_TO_REF
+    o = make_float4(fmaxf(0.0f, c.x - r.x), fmaxf(0.0f, c.y - r.y), fmaxf(0.0f, c.z - r.z), fmaxf(0.0f, c.w - r.w));
+  } else {                   // COMPARE_LUMINANCE: red = output brighter, green = reference brighter
+    const float lc = (c.x * (1.0f / 3.0f) + c.y * (1.0f / 3.0f)) + c.z * (1.0f / 3.0f);
+    const float lr = (r.x * (1.0f / 3.0f) + r.y * (1.0f / 3.0f)) + r.z * (1.0f / 3.0f);
+    o = make_float4(fmaxf(0.0f, lc - lr), fmaxf(0.0f, lr - lc), 0.0f, 1.0f);
+  }
+  out[i] = make_float4(o.x * scale, o.y * scale, o.z * scale, o.w * scale);
+}
+
+hipError_t launch_display(const float4* image, const float4* reference, float4* out, uint32_t n, uint32_t flags,
+                          float compare_scale, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  display_kernel<<<dim3(blocks_for(n)), dim3(kBlock), 0, s>>>(image, reference, out, n, flags, compare_scale);
+  return hipGetLastError();
+}
+
 // owned-tile pack/unpack for the multi-GPU exchange (renderer.cpp
 // mrt_tiles_pack / mrt_tiles_unpack): packed index = k * 4096 + ty * 64 + tx
 // for the k-th owned tile (global tile rank + k * count, row-major tiles)

@@ -118,6 +118,7 @@ struct mrt_renderer {
   uint32_t tiles_x = 0, tiles_y = 0, owned_tiles = 0;
   uint64_t owned_pixels = 0;
   std::vector<FrameSlot> slots;
+  uint32_t max_frames = 0;   // MAX_FRAMES (0 = unlimited)
   uint32_t inflight = 1;   // frames in flight (MRT_INFLIGHT): with dynamic work distribution and
                            // 8-frame batches one stream is as fast as 3 (C2) and launches do not overlap
   DevBuf counters;          // per (frame, bounce) survivor totals (stats)
@@ -360,6 +361,16 @@ int mrt_shard_mask(uint32_t W, uint32_t H, uint32_t rank, uint32_t count, uint8_
     }
   (void)ty_n;
   if (owned) *owned = n;
+  return MRT_OK;
+}
+
+int mrt_display(const float* image, const float* reference, float* out, uint32_t W, uint32_t H, uint32_t flags,
+                float compare_scale, void* stream) {
+  const uint32_t mode = (flags >> 8) & 0xFFu;
+  if (!image || !out || W == 0 || H == 0 || mode > 4 || (mode && !reference) || (flags & ~0xFF03u))
+    return fail(MRT_ERR_INVALID, "mrt_display: bad argument");
+  HIP_TRY(mrt::fast::launch_display(reinterpret_cast<const float4*>(image), reinterpret_cast<const float4*>(reference),
+                                    reinterpret_cast<float4*>(out), W * H, flags, compare_scale, (hipStream_t)stream));
   return MRT_OK;
 }
 
@@ -919,6 +930,8 @@ int mrt_renderer_prepare(mrt_renderer* r, uint32_t n) {
 
 int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  if (r->max_frames)   // MAX_FRAMES: renderer/Renderer.mm:589-590
+    n = r->frame_index >= r->max_frames ? 0u : (uint32_t)std::min<uint64_t>(n, r->max_frames - r->frame_index);
   if (n == 0) return MRT_OK;
   int rc = finalize_pending(r);
   if (rc) return rc;
@@ -1018,6 +1031,12 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
 }
 
 int mrt_renderer_draw(mrt_renderer* r) { return mrt_renderer_draw_n(r, 1); }
+
+int mrt_renderer_set_max_frames(mrt_renderer* r, uint32_t max_frames) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  r->max_frames = max_frames;
+  return MRT_OK;
+}
 
 int mrt_renderer_sync(mrt_renderer* r) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");

@@ -121,7 +121,7 @@ EXPORTED = [
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
     "mrt_debug_stamps", "mrt_shard_mask",
-    "mrt_tiles_packed_floats", "mrt_tiles_pack", "mrt_tiles_unpack",
+    "mrt_tiles_packed_floats", "mrt_tiles_pack", "mrt_tiles_unpack", "mrt_display", "mrt_renderer_set_max_frames",
     "mrt_accel_create", "mrt_accel_rebuild", "mrt_accel_intersect", "mrt_accel_info_get", "mrt_accel_destroy",
 ]
 
@@ -172,6 +172,8 @@ def lib() -> ctypes.CDLL:
         "mrt_debug_stamps": [vp, c_int],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
         "mrt_tiles_packed_floats": [u32, u32, u32, u32, ctypes.POINTER(u64)],
+        "mrt_display": [vp, vp, vp, u32, u32, u32, ctypes.c_float, vp],
+        "mrt_renderer_set_max_frames": [vp, u32],
         "mrt_tiles_pack": [vp, u32, u32, u32, u32, vp, vp],
         "mrt_tiles_unpack": [vp, u32, u32, u32, u32, vp, vp],
         "mrt_accel_create": [ctypes.POINTER(AccelDesc), ctypes.POINTER(vp)],
@@ -327,6 +329,10 @@ class Renderer:
     def draw(self, frames: int = 1) -> None:
         _check(lib().mrt_renderer_draw_n(self._h, frames), "mrt_renderer_draw_n")
 
+    def set_max_frames(self, n: int) -> None:
+        """MAX_FRAMES (Renderer.mm:589-590): draws past frame n are no-ops (0 = unlimited)."""
+        _check(lib().mrt_renderer_set_max_frames(self._h, n), "mrt_renderer_set_max_frames")
+
     def sync(self) -> None:
         _check(lib().mrt_renderer_sync(self._h), "mrt_renderer_sync")
 
@@ -428,6 +434,22 @@ def shard_mask(width: int, height: int, rank: int, count: int):
     _check(lib().mrt_shard_mask(width, height, rank, count, ctypes.c_void_p(m.ctypes.data),
                                 ctypes.c_void_p(n.ctypes.data)), "mrt_shard_mask")
     return m, int(n[0])
+
+
+DISPLAY_TONEMAP, DISPLAY_SRGB = 1, 2
+
+
+def display_compare(mode: int) -> int:
+    return mode << 8
+
+
+def display(image_ptr: int, out_ptr: int, width: int, height: int, flags: int = 0, reference_ptr: int | None = None,
+            compare_scale: float = 10.0, stream=None, sync=True) -> None:
+    """blitFragment (Shaders.metal:33-70): tone map / sRGB / golden comparison on the device."""
+    _check(lib().mrt_display(image_ptr, reference_ptr, out_ptr, width, height, flags, compare_scale, stream),
+           "mrt_display")
+    if sync:
+        synchronize(stream)
 
 
 def tiles_packed_floats(width: int, height: int, rank: int, count: int) -> int:

@@ -182,3 +182,42 @@ def resolve(isect, rays, srays):
 
 def accumulate(frame_index, rays, image):
     lib().orc_accumulate(len(rays), frame_index, _p(rays), _p(image))
+
+
+def to_srgb(v: np.ndarray) -> np.ndarray:
+    """toSRGB — renderer/Raytracing.h:130-135 (float32)."""
+    v = v.astype(np.float32)
+    lin = np.float32(12.92) * v
+    gam = np.float32(1.055) * np.power(np.maximum(v, np.float32(0)), np.float32(1.0 / 2.4)) - np.float32(0.055)
+    out = np.where(v < np.float32(0.0031308), lin, gam)
+    return np.where(v <= 0, np.float32(0), np.where(v >= 1, np.float32(1), out)).astype(np.float32)
+
+
+def display(image: np.ndarray, reference: np.ndarray | None, flags: int, scale: float) -> np.ndarray:
+    """blitFragment — renderer/Shaders.metal:33-70 (ENABLE_TONE_MAPPING = flags & 1,
+    MANUAL_SRGB = flags & 2, COMPARISON_MODE = flags >> 8, COMPARISON_SCALE = scale)."""
+    def blit(c):
+        c = c.astype(np.float32)
+        if flags & 1:
+            c = (np.float32(1) - np.exp(-c)).astype(np.float32)          # Shaders.metal:44-46
+        if flags & 2:
+            c = c.copy()
+            c[..., :3] = to_srgb(c[..., :3])                               # Shaders.metal:48-52
+        return c
+    c = blit(image)
+    mode = (flags >> 8) & 0xFF
+    if mode == 0:
+        return c
+    r = blit(reference)
+    if mode == 1:
+        o = np.abs(c - r)                                                  # :54-56
+    elif mode == 2:
+        o = np.maximum(0, r - c)                                           # :57-59
+    elif mode == 3:
+        o = np.maximum(0, c - r)                                           # :60-62
+    else:
+        k = np.float32(1.0 / 3.0)                                          # :63-67
+        lc = (c[..., 0] * k + c[..., 1] * k) + c[..., 2] * k
+        lr = (r[..., 0] * k + r[..., 1] * k) + r[..., 2] * k
+        o = np.stack([np.maximum(0, lc - lr), np.maximum(0, lr - lc), np.zeros_like(lc), np.ones_like(lc)], -1)
+    return (o * np.float32(scale)).astype(np.float32)

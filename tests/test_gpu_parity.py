@@ -256,3 +256,37 @@ def test_tiles_pack_unpack(gpu, mrt_mod, W, H, count):
         assert got.tobytes() == mrt_mod.tiles_pack_host(img, k, count).tobytes()
         mrt_mod.tiles_unpack(dev_ptr(d_p), W, H, k, count, dev_ptr(d_out))
     assert from_dev(d_out, np.float32).tobytes() == img.tobytes()
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2, 3, 1 << 8, (2 << 8) | 2, (3 << 8) | 1, (4 << 8) | 3])
+def test_display_blit(gpu, mrt_mod, oracle_mod, flags):
+    """blitFragment (Shaders.metal:33-70) against its numpy restatement:
+    tone map, sRGB, and the four golden-comparison modes."""
+    rng = np.random.default_rng(flags)
+    H, W = 37, 53
+    img = (rng.standard_normal((H, W, 4)) * 2).astype(np.float32)
+    ref = np.abs(rng.standard_normal((H, W, 4))).astype(np.float32)
+    d_img, d_ref, d_out = to_dev(img), to_dev(ref), to_dev(np.zeros_like(img))
+    mrt_mod.display(dev_ptr(d_img), dev_ptr(d_out), W, H, flags, reference_ptr=dev_ptr(d_ref) if flags >> 8 else None)
+    got = from_dev(d_out, np.float32).reshape(H, W, 4)
+    want = oracle_mod.display(img, ref, flags, 10.0)
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-5)
+
+
+def test_max_frames(gpu, mrt_mod):
+    """MAX_FRAMES (Renderer.mm:589-590): draws past the limit change nothing."""
+    sc = _scene(mrt_mod, "cornellbox")
+    r = mrt_mod.Renderer(sc, 64, 48, 2)
+    r.set_max_frames(3)
+    r.draw(2)
+    r.draw(5)
+    a = r.read_image()
+    st = r.stats()
+    r.draw(1)
+    b = r.read_image()
+    r.close()
+    r2 = mrt_mod.Renderer(sc, 64, 48, 2)
+    r2.draw(3)
+    c = r2.read_image()
+    r2.close()
+    assert st["frame_index"] == 3 and a.tobytes() == b.tobytes() == c.tobytes()
