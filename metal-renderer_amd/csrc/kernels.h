@@ -55,10 +55,13 @@ struct BounceArgs {
   uint32_t num_slots;          // per frame: owned tiles * 4096 pixel slots (bounce 0 input = num_slots * batch)
   uint32_t debug;              // ablation bits for profiling (0 in production, env MRT_DEBUG):
                                //   1 = skip shadow traversal, 2 = skip shading, 4 = no queue writes,
-                               //   8 = static interleaved work assignment (no grab counters)
-  // segmented queues: block g of a launch appends its survivors to slots
-  // [g*cap, g*cap + count_g) of the output queue (cap = chunk + kSegSlack)
-  uint32_t in_segments;        // bounce > 0: number of input segments (previous grid size)
+                               //   8 = static interleaved work assignment (no grab counters),
+                               //   16 = no material partition of the survivors
+  // segmented queues: block g of a launch appends its class-0 survivors
+  // (left a diffuse surface) to [g*cap, g*cap + c0_g) and its class-1
+  // survivors to [g*cap + cap - c1_g, g*cap + cap) of the output queue
+  // (cap = chunk + kSegSlack); counts are [c0 of all blocks][c1 of all blocks]
+  uint32_t in_segments;        // bounce > 0: number of input segments (2 x previous grid size)
   const uint32_t* in_seg_count;
   const uint32_t* in_chunk;    // previous launch's chunk (segment stride in slots)
   uint32_t* out_seg_count;     // [grid]

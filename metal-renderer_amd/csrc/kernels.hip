@@ -881,13 +881,13 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n
 template <int STACK, int MODE, int WIDTH>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
-  __shared__ uint32_t s_cursor, s_res;
+  __shared__ uint32_t s_cursor[2], s_res;
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
   const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1, a.stack_spill);
   uint32_t* seg = lds_u32() + cx.scratch_base;   // exclusive prefix of the input segments
-  if (tid == 0) s_cursor = s_res = 0;
+  if (tid == 0) s_cursor[0] = s_cursor[1] = s_res = 0;
 
   uint32_t N, in_chunk = 0;
   if (a.bounce == 0) {
@@ -897,6 +897,8 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     for (uint32_t i = tid; i < nseg; i += kBlock) seg[i] = a.in_seg_count[i];
     __syncthreads();
     N = block_exclusive_scan(seg, nseg, s_wave);
+    if (tid == 0) seg[nseg] = N;   // sentinel: count of segment j = seg[j+1] - seg[j]
+    __syncthreads();
     in_chunk = *a.in_chunk;
   }
   const uint32_t chunk = ((N + G - 1) / G + kBlock - 1) / kBlock * kBlock;
@@ -977,7 +979,11 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
       } else {
         uint32_t lo = 0, hi = nseg;   // last j with seg[j] <= idx
         while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
-        slot = lo * in_chunk + (idx - seg[lo]);
+        // segments [0, G): class 0 from the start of block j's range;
+        // [G, 2G): class 1, packed at the end of block j - G's range
+        const uint32_t g_in = nseg >> 1;
+        slot = lo < g_in ? lo * in_chunk + (idx - seg[lo])
+                         : (lo - g_in) * in_chunk + in_chunk - (seg[lo + 1] - seg[lo]) + (idx - seg[lo]);
         // planes 2-3 (throughput, pdf, radiance, ior) are loaded after the
         // traversal: they are not needed there, and keeping them out of the
         // traversal's live set saves 8 VGPRs
@@ -1036,19 +1042,30 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     //    is not live across it; plane 3 (radiance, ior) after it.
     if (active && (!hit_ok || last)) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
     const bool alive = hit_ok && !last;
-    const uint64_t mask = __ballot(alive);
+    // re-sort by material between bounces: survivors that left a diffuse
+    // surface (class 0) fill the block's segment from the front, the others
+    // (mirror / plastic / dielectric: specular and refracted rays) from the
+    // back; the next launch reads all class-0 segments first, so its waves
+    // see rays of one class (MRT_DEBUG bit 16: no partition)
+    const bool cls1 = (s.prevDiffuse == 0.0f) && !(a.debug & 16u);
+    const uint64_t mask0 = __ballot(alive && !cls1), mask1 = __ballot(alive && cls1);
     uint32_t o = 0;
-    if (mask) {
-      uint32_t wbase = 0;
-      if (lane == 0) wbase = atomicAdd(&s_cursor, (uint32_t)__popcll(mask));
-      wbase = __shfl(wbase, 0);
-      o = out_base + wbase + (uint32_t)__popcll(mask & lanes_below);
+    if (mask0 | mask1) {
+      uint32_t w0 = 0, w1 = 0;
+      if (lane == 0) {
+        if (mask0) w0 = atomicAdd(&s_cursor[0], (uint32_t)__popcll(mask0));
+        if (mask1) w1 = atomicAdd(&s_cursor[1], (uint32_t)__popcll(mask1));
+      }
+      w0 = __shfl(w0, 0);
+      w1 = __shfl(w1, 0);
+      o = cls1 ? out_base + cap - 1u - (w1 + (uint32_t)__popcll(mask1 & lanes_below))
+               : out_base + w0 + (uint32_t)__popcll(mask0 & lanes_below);
       if (alive && !(a.debug & 4u)) {
         a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
         a.out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
         a.out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
       }
-      wrote += (uint32_t)__popcll(mask);
+      wrote += (uint32_t)__popcll(mask0 | mask1);
     }
     STAMP(3);
     // -- phase 4: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
@@ -1063,8 +1080,10 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   STAMP_FLUSH();
   __syncthreads();
   if (tid == 0) {
-    a.out_seg_count[blockIdx.x] = s_cursor;
-    if (s_cursor) atomicAdd(a.out_total, s_cursor);   // stats: one atomic per block per launch
+    a.out_seg_count[blockIdx.x] = s_cursor[0];
+    a.out_seg_count[G + blockIdx.x] = s_cursor[1];
+    const uint32_t total = s_cursor[0] + s_cursor[1];
+    if (total) atomicAdd(a.out_total, total);   // stats: one atomic per block per launch
     if (blockIdx.x == 0) *a.out_chunk = cap;
   }
 }
@@ -1202,7 +1221,7 @@ int choose_mode(const DeviceScene& sc) {
 size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
   const size_t scene = (size_t)lds_scene_float4s(mode, 2 * sc.width, sc.num_nodes, sc.lds_nodes, sc.num_triangles,
                                                  sc.num_materials, sc.num_lights + 1) * 16;
-  const size_t scratch = ((size_t)grid + 1 + 3) / 4 * 16;
+  const size_t scratch = ((size_t)2 * grid + 1 + 3) / 4 * 16;   // 2 segments per block + sentinel
   return scene + scratch + (size_t)stack * kBlock * 4;   // stack = LDS entries (|STACK|)
 }
 
@@ -1230,13 +1249,20 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* gri
   hipDeviceProp_t prop;
   e = hipGetDeviceProperties(&prop, dev);
   if (e != hipSuccess) return e;
-  // the scratch depends on the grid: size with the worst case (8 blocks/CU)
-  const uint32_t worst_grid = (uint32_t)prop.multiProcessorCount * 8;
-  const DeviceScene f = fit_lds_nodes(sc, MODE, STACK < 0 ? -STACK : STACK, worst_grid);
-  const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, worst_grid);
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bounce_kernel<STACK, MODE, WIDTH>, kBlock, lds) != hipSuccess || n <= 0)
-    n = 1;
+  // the LDS scratch (2 segment counts per block) depends on the grid: take
+  // the largest blocks/CU n whose own LDS footprint still allows n resident
+  // blocks (and the VGPR budget allows)
+  const uint32_t cus = (uint32_t)prop.multiProcessorCount;
+  const int stack = STACK < 0 ? -STACK : STACK;
+  int n = 1;
+  for (int want = 8; want >= 1; --want) {
+    const uint32_t g = cus * (uint32_t)want;
+    const size_t lds = bounce_lds_bytes(fit_lds_nodes(sc, MODE, stack, g), MODE, stack, g);
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bounce_kernel<STACK, MODE, WIDTH>, kBlock, lds) != hipSuccess)
+      occ = 0;
+    if (occ >= want) { n = want; break; }
+  }
   // one launch at a time: every resident block slot (the dynamic work
   // distribution leaves no tail to fill); with frames in flight the caller
   // asks for fewer blocks per CU per launch
@@ -1282,6 +1308,7 @@ hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_e
     return dispatch_width<-32>(sc, a, grid, grid_out, s);
   }
   if (stack_entries <= 8) return dispatch_width<8>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 12) return dispatch_width<12>(sc, a, grid, grid_out, s);
   if (stack_entries <= 16) return dispatch_width<16>(sc, a, grid, grid_out, s);
   if (stack_entries <= 24) return dispatch_width<24>(sc, a, grid, grid_out, s);
   return dispatch_width<32>(sc, a, grid, grid_out, s);

@@ -230,7 +230,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
   // slack of the segments (kernels.h)
   const size_t slots = owned_slots * r->batch + (size_t)r->grid * (256 + mrt::kSegSlack);
   for (FrameSlot& fs : r->slots) {
-    HIP_TRY(fs.segments.alloc(((size_t)2 * r->grid + 2) * 4));
+    HIP_TRY(fs.segments.alloc(((size_t)4 * r->grid + 2) * 4));   // 2 queues x 2 classes x grid + 2 chunk words
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(slots * 16));
@@ -874,7 +874,7 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   uint32_t cap = need <= 16 ? 16 : 8;
   if (const char* v = std::getenv("MRT_STACK")) cap = std::max<uint32_t>(8, (uint32_t)std::strtoul(v, nullptr, 0));
   const uint32_t want = std::min(need, cap);
-  r->stack_entries = want <= 8 ? 8 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
+  r->stack_entries = want <= 8 ? 8 : want <= 12 ? 12 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
   if (need > r->stack_entries) r->stack_entries = r->stack_entries <= 8 ? 8 : r->stack_entries <= 16 ? 16 : 32;   // spill variants
   if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
   if (const char* v = std::getenv("MRT_PROFILE_EVERY"))
@@ -965,7 +965,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     const uint32_t batch = std::min<uint32_t>(B, n - k * B);
     FrameSlot& fs = r->slots[k % r->inflight];
     uint32_t* seg = fs.segments.as<uint32_t>();
-    uint32_t* meta = seg + 2 * (size_t)r->grid;
+    uint32_t* meta = seg + 4 * (size_t)r->grid;
     for (uint32_t b = 0; b < L; ++b) {
       mrt::BounceArgs a{};
       a.width = r->desc.width;
@@ -979,10 +979,10 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.tiles_x = r->tiles_x;
       a.num_slots = r->owned_tiles * 4096u;
       a.debug = r->debug;
-      a.in_segments = r->grid;
-      a.in_seg_count = seg + (size_t)((b + 1) & 1) * r->grid;
+      a.in_segments = 2 * r->grid;   // two material classes per block
+      a.in_seg_count = seg + (size_t)((b + 1) & 1) * 2 * r->grid;
       a.in_chunk = meta + ((b + 1) & 1);
-      a.out_seg_count = seg + (size_t)(b & 1) * r->grid;
+      a.out_seg_count = seg + (size_t)(b & 1) * 2 * r->grid;
       a.out_chunk = meta + (b & 1);
       a.out_total = cnt + (size_t)k * L + b;
       a.grab = r->grabs.as<uint32_t>() + ((size_t)k * L + b) * grab_words;
