@@ -9,7 +9,7 @@ accumulation image to rank 0.  value = paths of all ranks / max-over-ranks
 step time (strong scaling: the frame is split into 64x64 tiles, tile t on
 rank t % N).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3g|c4|c5]
 For N > 1 launch with torch.distributed.run (one process per GPU).
 --shard-of S (N = 1 only): render only rank 0's tiles of an S-way split —
 one GPU's share of a multi-GPU job, value = that share's paths/s (diagnostic).
@@ -36,6 +36,12 @@ CONFIGS = {
     # configs[2]: CornellBox-Water-plastic (plastic + mirror + water), 256 spp, L = 8
     "c3": dict(workload="C3 CornellBox-Water-plastic 1920x1080 256spp L=8", scene="CornellBox-Water-plastic",
                mtl=None, width=1920, height=1080, spp=256, L=8, procedural=0),
+    # configs[2] with the generated "glass" variant: the water
+    # becomes a dielectric (Ks 0 0 +1.33333), so diffuse walls, the mirror
+    # sphere, the plastic sphere and the dielectric water exercise all 4 BSDFs
+    "c3g": dict(workload="C3 CornellBox-Water-plastic + glass water 1920x1080 256spp L=8 (all 4 BSDFs)",
+                scene="CornellBox-Water-plastic", mtl="glass-water", width=1920, height=1080, spp=256, L=8,
+                procedural=0),
     # configs[3]: 1M-triangle procedural mesh in the cornellbox shell, 64 spp, L = 4
     "c4": dict(workload="C4 1M-triangle procedural mesh 1920x1080 64spp L=4", scene="cornellbox", mtl=None,
                width=1920, height=1080, spp=64, L=4, procedural=1 << 20),
@@ -70,6 +76,20 @@ def parse():
     return p.parse_args()
 
 
+def resolve_mtl(cfg):
+    """Material override of a config: None (the OBJ's own mtllib) or a
+    generated variant written next to the run's outputs."""
+    if cfg["mtl"] != "glass-water":
+        return cfg["mtl"]
+    import tempfile
+    import mrt
+    src = open(mrt.scene_path(cfg["scene"])[:-4] + ".mtl").read()
+    out = os.path.join(tempfile.gettempdir(), f"mrt-{os.getpid()}-glass-water.mtl")
+    with open(out, "w") as f:
+        f.write(src.replace("Ks 0.0 0.0 -1.33333", "Ks 0.0 0.0 1.33333"))
+    return out
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -86,8 +106,8 @@ def cpu_baseline(cfg, frames):
     nearest hit in place of MPS) timed on this host on a bounded sample of the
     same workload: C2 runs in full (all `frames` = spp frames
     of the whole image) on `threads` std::threads over rows, and 2 frames on
-    one thread give the scalar rate.  Scenes with more triangles run a row
-    band sized to keep the sample within ~10-30 s."""
+    one thread give the scalar rate.  Scenes with more triangles run one frame
+    of a row band sized to ~10 s on all threads and ~10 s on one."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle  # test/baseline infrastructure only (see oracle/mrt_oracle.cpp header)
@@ -97,10 +117,21 @@ def cpu_baseline(cfg, frames):
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
     if cfg["procedural"]:
         return None   # brute force over 1M triangles is not a bounded sample
-    sc = oracle.OracleScene(mrt.scene_path(cfg["scene"]), cfg["mtl"])
+    sc = oracle.OracleScene(mrt.scene_path(cfg["scene"]), resolve_mtl(cfg))
     W, H = cfg["width"], cfg["height"]
-    # brute force costs ~ triangles: keep ~16 M triangle-tests x bounces per thread-second budget
-    rows = H if sc.n_triangles <= 64 else max(8, min(H, int(H * 64 / sc.n_triangles * 8)))
+    if sc.n_triangles <= 64:
+        rows = H                      # C2: the whole workload (all spp frames)
+        rows1 = H
+        f1 = min(2, frames)
+    else:
+        # brute force costs ~ (bounces x 2 traversals x triangles) tests per
+        # path at ~1.6e8 tests/s per thread: size the sample to ~10 s on all
+        # threads (one frame of a row band) and ~10 s on one thread
+        frames = 1
+        per_path = min(cfg["L"], 5) * 2 * sc.n_triangles
+        rows = max(1, min(H, int(10.0 * 1.6e8 * threads / (per_path * W))))
+        rows1 = max(1, rows // threads)
+        f1 = 1
     mask = np.zeros((H, W), np.uint8)
     y0 = (H - rows) // 2
     mask[y0:y0 + rows] = 1
@@ -108,17 +139,18 @@ def cpu_baseline(cfg, frames):
     sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads, pixel_mask=mask)
     dt = time.perf_counter() - t0
     paths = W * rows * frames
-    f1 = min(2, frames)
+    mask1 = np.zeros((H, W), np.uint8)
+    mask1[y0:y0 + rows1] = 1
     t1 = time.perf_counter()
-    sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, f1, threads=1, pixel_mask=mask)
+    sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, f1, threads=1, pixel_mask=mask1)
     dt1 = time.perf_counter() - t1
     return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "single_thread_value": round(W * rows * f1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
+            "single_thread_value": round(W * rows1 * f1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
             "cpu_model": _cpu_model(),
             "sample": f"frames 0-{frames - 1}, rows {y0}-{y0 + rows - 1} of the workload ({W}x{rows} of {W}x{H}, "
                       f"L={cfg['L']}, {paths} paths), brute-force nearest hit over {sc.n_triangles} triangles, "
                       f"{threads} std::threads over rows, {dt:.2f} s wall; single thread: frames 0-{f1 - 1} "
-                      f"of the same rows, {dt1:.2f} s"}
+                      f"of rows {y0}-{y0 + rows1 - 1}, {dt1:.2f} s"}
 
 
 def main():
@@ -147,7 +179,7 @@ def main():
         else:
             dist.init_process_group("gloo")
     W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
-    scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=device,
+    scene = mrt.Scene(cfg["scene"], resolve_mtl(cfg), procedural_triangles=cfg["procedural"], device=device,
                       bvh_builder={"sah": mrt.BVH_HOST_SAH, "lbvh": mrt.BVH_DEVICE_LBVH,
                                    "ploc": mrt.BVH_DEVICE_PLOC}[args.bvh])
     # the accumulation image lives in a torch tensor so RCCL can reduce it in

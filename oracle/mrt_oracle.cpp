@@ -724,8 +724,9 @@ void orc_accumulate(uint32_t count, uint32_t frameIndex, const void* rays, float
 
 // ---- whole-frame driver: performRaytracing: (renderer/Renderer.mm:500-585) --
 // Renders frames [frame_begin, frame_end) into image_rgba (W*H*4, row 0 =
-// bottom), accumulating as accumulateImage does.  Rows are split across
-// `threads` std::threads (pixels are independent within a frame).
+// bottom), accumulating as accumulateImage does.  Rows are handed out one at
+// a time to `threads` std::threads (pixels are independent within a frame;
+// a shared row counter keeps masked bands and uneven rows balanced).
 // active_out (optional) receives A = sum over iterations of rays alive at
 // the start of the iteration.  pixel_mask (optional, W*H bytes) restricts the
 // render to pixels with mask != 0 (others untouched) for bounded samples.
@@ -740,9 +741,10 @@ int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLeng
     const float* raygenNoise = nc.get(f);
     std::vector<const float*> iterNoise(maxPathLength);
     for (uint32_t i = 0; i < maxPathLength; ++i) iterNoise[i] = nc.get(noise_frame_for(f, i));
-    auto work = [&](uint32_t y0, uint32_t y1) {
+    std::atomic<uint32_t> next_row{0};
+    auto work = [&]() {
       uint64_t local = 0;
-      for (uint32_t y = y0; y < y1; ++y)
+      for (uint32_t y = next_row++; y < H; y = next_row++)
         for (uint32_t x = 0; x < W; ++x) {
           size_t pix = (size_t)y * W + x;
           if (pixel_mask && !pixel_mask[pix]) continue;
@@ -759,14 +761,10 @@ int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLeng
         }
       active += local;
     };
-    if (threads == 1) work(0, H);
+    if (threads == 1) work();
     else {
       std::vector<std::thread> th;
-      uint32_t chunk = (H + threads - 1) / threads;
-      for (uint32_t t = 0; t < threads; ++t) {
-        uint32_t y0 = t * chunk, y1 = std::min(H, y0 + chunk);
-        if (y0 < y1) th.emplace_back(work, y0, y1);
-      }
+      for (uint32_t t = 0; t < threads; ++t) th.emplace_back(work);
       for (auto& t : th) t.join();
     }
   }

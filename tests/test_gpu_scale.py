@@ -65,13 +65,22 @@ def test_deep_bvh_render_parity(proc_scenes, mrt_mod, monkeypatch, lds_stack):
     assert abs(st["active_ray_bounces"] - A) <= max(2, A // 1000)
 
 
-def test_glass_variant_parity(gpu, mrt_mod, oracle_mod, tmp_path):
+@pytest.mark.parametrize("variant", ["both", "water"])
+def test_glass_variant_parity(gpu, mrt_mod, oracle_mod, tmp_path, variant):
+    """The generated "glass" variants of C3 (no shipped MTL instantiates
+    DIELECTRIC): both transparent objects glass, or only the water (bench.py
+    c3g: diffuse + mirror + plastic + dielectric, all four BSDFs)."""
     src = open(mrt_mod.scene_path("CornellBox-Water-plastic")[:-4] + ".mtl").read()
     p = tmp_path / "glass.mtl"
-    p.write_text(src.replace("Ks 0.0 0.0 -1.5", "Ks 0.0 0.0 1.5").replace("Ks 0.0 0.0 -1.33333", "Ks 0.0 0.0 1.33333"))
+    txt = src.replace("Ks 0.0 0.0 -1.33333", "Ks 0.0 0.0 1.33333")
+    if variant == "both":
+        txt = txt.replace("Ks 0.0 0.0 -1.5", "Ks 0.0 0.0 1.5")
+    p.write_text(txt)
     sc = mrt_mod.Scene("CornellBox-Water-plastic", str(p))
     types = sc.export()["materials"]["materialType"]
-    assert (types == 3).sum() == 2
+    assert (types == 3).sum() == (2 if variant == "both" else 1)
+    if variant == "water":
+        assert set(types.tolist()) == {0, 1, 2, 3}
     osc = oracle_mod.OracleScene(mrt_mod.scene_path("CornellBox-Water-plastic"), str(p))
     W, H, L, frames = 48, 36, 8, 2
     ref, A = osc.render(W, H, L, SEED, frames, threads=8)

@@ -13,7 +13,7 @@ import mrt  # noqa: E402
 
 cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-scene = mrt.Scene(cfg["scene"], cfg["mtl"], procedural_triangles=cfg["procedural"], device=0)
+scene = mrt.Scene(cfg["scene"], bench.resolve_mtl(cfg), procedural_triangles=cfg["procedural"], device=0)
 r = mrt.Renderer(scene, cfg["width"], cfg["height"], cfg["L"])
 r.draw(8)
 r.sync()
