@@ -9,7 +9,7 @@ accumulation image to rank 0.  value = paths of all ranks / max-over-ranks
 step time (strong scaling: the frame is split into 64x64 tiles, tile t on
 rank t % N).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3g|c4|c5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c3g|c4|c5]
 For N > 1 launch with torch.distributed.run (one process per GPU).
 --shard-of S (N = 1 only): render only rank 0's tiles of an S-way split —
 one GPU's share of a multi-GPU job, value = that share's paths/s (diagnostic).
@@ -30,6 +30,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 B_PATH, B_BOUNCE = 112, 312    # algorithmic bytes per path / per active ray-bounce
 
 CONFIGS = {
+    # BASELINE.json configs[0]: the reference's CPU-runnable plumbing case (also on the GPU)
+    "c1": dict(workload="C1 cornellbox 256x256 1spp L=1", scene="cornellbox", mtl=None,
+               width=256, height=256, spp=1, L=1, procedural=0),
     # BASELINE.json configs[1] — the metric's config
     "c2": dict(workload="C2 cornellbox 1920x1080 64spp L=4 (diffuse BSDF)", scene="cornellbox", mtl=None,
                width=1920, height=1080, spp=64, L=4, procedural=0),
@@ -315,7 +318,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames or (spp if args.config == "c2" else 8))
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames or (spp if args.config in ("c1", "c2") else 8))
     if world > 1 and args.check_image:
         if rank == 0:   # the exchanged image == one device rendering the whole frame, bitwise
             ref = torch.zeros_like(image)
