@@ -200,6 +200,19 @@ int main(int argc, char** argv) {
           R rr{h, r, 0, trace(b, h, r).steps};
           rs.push_back(rr);
         }
+    for (int axis = 0; axis < 3; ++axis) {   // 1-bit keys: sign of one direction component, global 2-way partition
+      std::vector<R> v = rs;
+      std::stable_sort(v.begin(), v.end(), [&](const R& a, const R& c) {
+        const float da = axis == 0 ? a.d.x : axis == 1 ? a.d.y : a.d.z, dc = axis == 0 ? c.d.x : axis == 1 ? c.d.y : c.d.z;
+        return (da > 0) < (dc > 0); });
+      double li = 0, wi = 0;
+      for (size_t w0 = 0; w0 < v.size(); w0 += 64) {
+        int mx = 0;
+        for (size_t i = w0; i < std::min(v.size(), w0 + 64); ++i) { li += v[i].steps; mx = std::max(mx, v[i].steps); }
+        wi += 64.0 * mx;
+      }
+      std::printf("sorted secondaries: sign of d[%d] (global 2-way): SIMD efficiency %.3f\n", axis, li / wi);
+    }
     for (int keybits : {0, 3, 6}) {
       for (size_t S : {size_t(128), size_t(1024), size_t(8192), rs.size()}) {
         std::vector<R> v = rs;
