@@ -214,13 +214,14 @@ int alloc_frame_buffers(mrt_renderer* r) {
     const uint64_t h = std::min<uint32_t>(mrt::kTile, H - ty * mrt::kTile);
     r->owned_pixels += w * h;
   }
-  // frames per launch: about 2^24 rays per launch (8 frames at 1080p, 64
-  // frames of a 1/8 tile share), so the launch-boundary drain is a small share
-  // of each launch and a GPU that owns a small share of the tiles still
-  // issues full-size launches (1/8 share with 8-frame batches: 62 % of the
-  // per-GPU rate)
+  // frames per launch: about 2^27 rays per launch (64 frames at 1080p, up
+  // to kMaxBatch), so the launch-boundary drain (the last grabs finishing at
+  // falling occupancy, ~20-40 us) is a small share of each launch: C2 at
+  // 2^24 rays per launch (8 frames) 5210, 2^25 5431, 2^26 5551, 2^27 5617
+  // Mpaths/s.  Memory: 64 B per queued ray x 2 queues + 16 B radiance
+  // (~19.5 GB at 2^27 rays, of 288 GB).
   const size_t owned_slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096);
-  r->batch = (uint32_t)std::min<size_t>(mrt::kMaxBatch, std::max<size_t>(1, ((size_t)1 << 24) / owned_slots));
+  r->batch = (uint32_t)std::min<size_t>(mrt::kMaxBatch, std::max<size_t>(1, ((size_t)1 << 27) / owned_slots));
   if (const char* v = std::getenv("MRT_BATCH"))
     r->batch = std::max<uint32_t>(1, std::min<uint32_t>(mrt::kMaxBatch, (uint32_t)std::strtoul(v, nullptr, 0)));
   // a ray's tag holds batch * owned slots in 31 bits
