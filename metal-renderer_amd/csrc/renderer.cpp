@@ -93,6 +93,18 @@ struct mrt_scene {
   mrt_scene_info info{};
 };
 
+// bookkeeping of one draw_n call whose statistics are not read back yet
+struct DrawRecord {
+  DevBuf counters;                          // per (batch, bounce) survivor totals
+  hipEvent_t start = nullptr, stop = nullptr;
+  std::vector<hipEvent_t> kernel_events;    // MRT_FLAG_PROFILE: 2 per timed bounce launch
+  uint32_t frames = 0;
+  uint32_t launches = 0;                    // batches (bounce launches = batches * L)
+  size_t events = 0;
+  bool pending = false;
+};
+constexpr int kDrawRing = 3;
+
 // One in-flight frame: its queues, segment counts, per-pixel path radiance and
 // the stream its bounce launches run on.  Frames f and f+1 run on different
 // slots concurrently (the reference keeps up to 3 frames in flight,
@@ -121,22 +133,20 @@ struct mrt_renderer {
   uint32_t max_frames = 0;   // MAX_FRAMES (0 = unlimited)
   uint32_t inflight = 1;   // frames in flight (MRT_INFLIGHT): with dynamic work distribution and
                            // 8-frame batches one stream is as fast as 3 (C2) and launches do not overlap
-  DevBuf counters;          // per (frame, bounce) survivor totals (stats)
   DevBuf grabs;             // per (launch) grab counters of the dynamic work distribution
   uint32_t grid = 0;        // persistent grid of the bounce kernel
   // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
   DevBuf noise_init, noise_window;
   int64_t noise_first = 0, noise_count = 0;
   uint64_t frame_index = 0;
-  // pending draw bookkeeping
-  bool pending = false;
-  uint32_t pending_frames = 0;
-  uint32_t pending_launches = 0;   // batches of the pending draw (bounce launches = batches * L)
-  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-  std::vector<hipEvent_t> kernel_events;   // MRT_FLAG_PROFILE: 2 per timed bounce launch
-  uint32_t profile_every = 8;
-  uint32_t batch = 1;                       // frames per bounce launch (frame batching)               // time the launches of every n-th frame (MRT_PROFILE_EVERY)
-  size_t pending_events = 0;
+  // Draws in flight: each draw records its survivor counters and events in
+  // its own ring entry, and its statistics are read back lazily (when the
+  // entry is reused, or on stats / sync / read), so consecutive draws queue
+  // back to back without a host round trip between them.
+  DrawRecord draws[kDrawRing];
+  uint32_t draw_next = 0;   // ring entry of the next draw (= the oldest pending one)
+  uint32_t profile_every = 8;   // time the launches of every n-th batch (MRT_PROFILE_EVERY)
+  uint32_t batch = 1;           // frames per bounce launch (frame batching)
   mrt_stats stats{};
   uint32_t stack_entries = 32;
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
@@ -144,31 +154,40 @@ struct mrt_renderer {
 
 namespace {
 
-int finalize_pending(mrt_renderer* r) {
-  if (!r->pending) return MRT_OK;
-  HIP_TRY(hipEventSynchronize(r->ev_stop));
+int finalize_draw(mrt_renderer* r, DrawRecord& d) {
+  if (!d.pending) return MRT_OK;
+  HIP_TRY(hipEventSynchronize(d.stop));
   float ms = 0.0f;
-  HIP_TRY(hipEventElapsedTime(&ms, r->ev_start, r->ev_stop));
+  HIP_TRY(hipEventElapsedTime(&ms, d.start, d.stop));
   const uint32_t L = r->desc.max_path_length;
-  std::vector<uint32_t> cnt((size_t)r->pending_launches * L);
-  HIP_TRY(hipMemcpy(cnt.data(), r->counters.p, cnt.size() * 4, hipMemcpyDeviceToHost));
-  uint64_t active = r->owned_pixels * r->pending_frames;   // bounce 0: every owned pixel's camera ray
-  for (uint32_t k = 0; k < r->pending_launches; ++k)
+  std::vector<uint32_t> cnt((size_t)d.launches * L);
+  HIP_TRY(hipMemcpy(cnt.data(), d.counters.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+  uint64_t active = r->owned_pixels * d.frames;   // bounce 0: every owned pixel's camera ray
+  for (uint32_t k = 0; k < d.launches; ++k)
     for (uint32_t b = 0; b + 1 < L; ++b) active += cnt[(size_t)k * L + b];
   r->stats.active_ray_bounces += active;
   r->stats.last_draw_ms = ms;
-  const uint64_t paths = r->owned_pixels * r->pending_frames;
+  const uint64_t paths = r->owned_pixels * d.frames;
   r->stats.mpaths_per_s = ms > 0.0f ? (double)paths / (ms * 1e-3) / 1e6 : 0.0;
-  r->stats.kernel_launches += (uint64_t)r->pending_launches * L;
+  r->stats.kernel_launches += (uint64_t)d.launches * L;
   if (r->desc.flags & MRT_FLAG_PROFILE) {
-    for (size_t k = 0; k + 1 < r->pending_events; k += 2) {
+    for (size_t k = 0; k + 1 < d.events; k += 2) {
       float ms_k = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&ms_k, r->kernel_events[k], r->kernel_events[k + 1]));
+      HIP_TRY(hipEventElapsedTime(&ms_k, d.kernel_events[k], d.kernel_events[k + 1]));
       r->stats.kernel_ms += ms_k;
       r->stats.timed_launches += 1;
     }
   }
-  r->pending = false;
+  d.pending = false;
+  return MRT_OK;
+}
+
+// read back every pending draw, oldest first
+int finalize_pending(mrt_renderer* r) {
+  for (int i = 0; i < kDrawRing; ++i) {
+    const int rc = finalize_draw(r, r->draws[(r->draw_next + i) % kDrawRing]);
+    if (rc) return rc;
+  }
   return MRT_OK;
 }
 
@@ -192,7 +211,7 @@ int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
         mrt::make_noise_table(r->desc.seed, lo + k < 0 ? -1 : lo + k, host.data() + (size_t)k * mrt::kNoiseFloats);
     });
   for (auto& x : th) x.join();
-  if (r->pending) { int rc = finalize_pending(r); if (rc) return rc; }
+  { int rc = finalize_pending(r); if (rc) return rc; }
   HIP_TRY(hipStreamSynchronize(r->stream));
   HIP_TRY(upload(r->noise_window, host.data(), host.size() * 4));
   r->noise_first = lo;
@@ -864,8 +883,10 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   }
   r->own_image = desc->image == nullptr;
   r->image = desc->image;
-  HIP_TRY(hipEventCreate(&r->ev_start));
-  HIP_TRY(hipEventCreate(&r->ev_stop));
+  for (DrawRecord& d : r->draws) {
+    HIP_TRY(hipEventCreate(&d.start));
+    HIP_TRY(hipEventCreate(&d.stop));
+  }
   // LDS stack capacity: the BVH's bound rounded up to 8/16 entries when it is
   // <= 16; deeper BVHs keep 8 entries in LDS and spill the rest to global
   // memory (MRT_STACK overrides the cap).  LDS per block bounds the resident
@@ -916,8 +937,7 @@ int mrt_renderer_resize(mrt_renderer* r, uint32_t width, uint32_t height) {
 
 int mrt_renderer_reset(mrt_renderer* r) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");
-  int rc = finalize_pending(r);
-  if (rc) return rc;
+  // stream-ordered after the pending draws: no read-back needed here
   HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)r->desc.width * r->desc.height * 16, r->stream));
   r->frame_index = 0;
   r->stats.frame_index = 0;   // cumulative counters (paths, A, kernel time) persist
@@ -934,7 +954,8 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   if (r->max_frames)   // MAX_FRAMES: renderer/Renderer.mm:589-590
     n = r->frame_index >= r->max_frames ? 0u : (uint32_t)std::min<uint64_t>(n, r->max_frames - r->frame_index);
   if (n == 0) return MRT_OK;
-  int rc = finalize_pending(r);
+  DrawRecord& d = r->draws[r->draw_next];
+  int rc = finalize_draw(r, d);   // the ring entry's previous draw (kDrawRing draws back)
   if (rc) return rc;
   rc = ensure_noise(r, (int64_t)r->frame_index, n);
   if (rc) return rc;
@@ -942,23 +963,23 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   const uint32_t B = r->batch;
   const uint32_t nb = (n + B - 1) / B;   // launches of up to B frames each
   const size_t counter_bytes = (size_t)nb * L * 4;
-  if (r->counters.bytes < counter_bytes) HIP_TRY(r->counters.alloc(counter_bytes));
-  HIP_TRY(hipMemsetAsync(r->counters.p, 0, counter_bytes, r->stream));
+  if (d.counters.bytes < counter_bytes) HIP_TRY(d.counters.alloc(counter_bytes));
+  HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, r->stream));
   const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
   if (r->grabs.bytes < (size_t)nb * L * grab_words * 4) HIP_TRY(r->grabs.alloc((size_t)nb * L * grab_words * 4));
   HIP_TRY(hipMemsetAsync(r->grabs.p, 0, (size_t)nb * L * grab_words * 4, r->stream));
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
     const size_t need = (size_t)2 * ((nb + r->profile_every - 1) / r->profile_every) * L;
-    while (r->kernel_events.size() < need) {
+    while (d.kernel_events.size() < need) {
       hipEvent_t e;
       HIP_TRY(hipEventCreate(&e));
-      r->kernel_events.push_back(e);
+      d.kernel_events.push_back(e);
     }
   }
-  HIP_TRY(hipEventRecord(r->ev_start, r->stream));
-  for (uint32_t k = 1; k < r->inflight; ++k) HIP_TRY(hipStreamWaitEvent(r->slots[k].stream, r->ev_start, 0));
-  uint32_t* cnt = r->counters.as<uint32_t>();
+  HIP_TRY(hipEventRecord(d.start, r->stream));
+  for (uint32_t k = 1; k < r->inflight; ++k) HIP_TRY(hipStreamWaitEvent(r->slots[k].stream, d.start, 0));
+  uint32_t* cnt = d.counters.as<uint32_t>();
   size_t ev = 0;
   const FrameSlot* prev = nullptr;
   for (uint32_t k = 0; k < nb; ++k) {
@@ -996,9 +1017,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.radiance = fs.radiance.as<float4>();
       a.stack_spill = fs.spill.as<uint32_t>();
       const bool timed = profile && (k % r->profile_every) == 0;
-      if (timed) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
+      if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
       HIP_TRY(launch_bounce(r, a, fs.stream));
-      if (timed) HIP_TRY(hipEventRecord(r->kernel_events[ev++], fs.stream));
+      if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
     }
     // accumulateImage for frames f .. f+batch-1, after the previous batch's
     // (running mean order)
@@ -1020,11 +1041,12 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   }
   // join every slot back into the main stream
   for (uint32_t k = 1; k < r->inflight && k < nb; ++k) HIP_TRY(hipStreamWaitEvent(r->stream, r->slots[k].acc_done, 0));
-  HIP_TRY(hipEventRecord(r->ev_stop, r->stream));
-  r->pending = true;
-  r->pending_frames = n;
-  r->pending_launches = nb;
-  r->pending_events = ev;
+  HIP_TRY(hipEventRecord(d.stop, r->stream));
+  d.pending = true;
+  d.frames = n;
+  d.launches = nb;
+  d.events = ev;
+  r->draw_next = (r->draw_next + 1) % kDrawRing;
   r->frame_index += n;
   r->stats.frame_index = r->frame_index;
   r->stats.paths += r->owned_pixels * n;
@@ -1094,9 +1116,11 @@ int mrt_renderer_destroy(mrt_renderer* r) {
     if (fs.own_stream) (void)hipStreamDestroy(fs.stream);
   }
   r->slots.clear();
-  for (hipEvent_t e : r->kernel_events) (void)hipEventDestroy(e);
-  if (r->ev_start) (void)hipEventDestroy(r->ev_start);
-  if (r->ev_stop) (void)hipEventDestroy(r->ev_stop);
+  for (DrawRecord& d : r->draws) {
+    for (hipEvent_t e : d.kernel_events) (void)hipEventDestroy(e);
+    if (d.start) (void)hipEventDestroy(d.start);
+    if (d.stop) (void)hipEventDestroy(d.stop);
+  }
   if (r->own_stream) (void)hipStreamDestroy(r->stream);
   delete r;
   return MRT_OK;
