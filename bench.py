@@ -207,6 +207,7 @@ def main():
 
     def exchange():
         r.sync()
+        torch.cuda.synchronize()   # the previous step's collective has released `packed` / `image`
         if args.exchange == "reduce":
             if args.dist_backend == "nccl":
                 dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
