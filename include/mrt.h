@@ -69,7 +69,7 @@ typedef struct mrt_scene_desc {
   const char* mtl_override;        /* optional .mtl used instead of the OBJ's mtllib (NULL/"" = none) */
   uint32_t procedural_triangles;   /* >0: append a seeded displaced sphere of this many triangles */
   uint64_t procedural_seed;
-  uint32_t max_leaf_size;          /* BVH leaf size, 0 = default (4) */
+  uint32_t max_leaf_size;          /* BVH leaf size, 0 = default (2) */
   uint32_t lds_nodes;              /* top BVH nodes staged in LDS, 0 = default; UINT32_MAX = none */
   int device;                      /* HIP device ordinal; -1 = host only (import + BVH, no upload) */
   uint32_t bvh_width;              /* 2 = BVH2, 4 = BVH4 (collapsed BVH2), 0 = default (4) */
@@ -119,7 +119,7 @@ typedef struct mrt_accel_desc {
   uint32_t triangle_count;
   int device;                      /* HIP device of the buffers */
   uint32_t builder;                /* MRT_BVH_*; 0 = default (MRT_BVH_DEVICE_PLOC) */
-  uint32_t max_leaf_size;          /* 0 = default (4) */
+  uint32_t max_leaf_size;          /* 0 = default (2) */
   void* stream;                    /* hipStream_t of libmrt's runtime, NULL = own stream */
 } mrt_accel_desc;
 typedef struct mrt_accel_info {

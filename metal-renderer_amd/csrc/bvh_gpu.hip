@@ -404,7 +404,7 @@ struct Tmp {
 hipError_t build_bvh_gpu(const float* positions, uint32_t stride_bytes, const uint32_t* indices, uint32_t T,
                          uint32_t max_leaf, GpuBvhAlgo algo, hipStream_t s, GpuBvhResult& out, std::string& error) {
   out = GpuBvhResult{};
-  max_leaf = std::max<uint32_t>(1, std::min<uint32_t>(max_leaf ? max_leaf : 4, (uint32_t)kMaxLeafSize));
+  max_leaf = std::max<uint32_t>(1, std::min<uint32_t>(max_leaf ? max_leaf : 2, (uint32_t)kMaxLeafSize));
   if (T >= (1u << (32 - kLeafCountBits - 1))) { error = "too many triangles for the leaf encoding"; return hipErrorInvalidValue; }
   hipEvent_t e0, e1;
   GB_TRY(hipEventCreate(&e0));

@@ -696,7 +696,7 @@ namespace {
 int accel_build(mrt_accel* a) {
   const mrt_accel_desc& d = a->desc;
   const uint32_t T = d.triangle_count;
-  const uint32_t leaf = d.max_leaf_size ? d.max_leaf_size : 4;
+  const uint32_t leaf = d.max_leaf_size ? d.max_leaf_size : 2;
   HIP_TRY(hipSetDevice(d.device));
   hipStream_t s = (hipStream_t)d.stream;
   std::string err;
