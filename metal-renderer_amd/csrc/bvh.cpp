@@ -106,10 +106,41 @@ struct Builder {
         if (cost < best_cost) { best_cost = cost; best_axis = axis; best_split = b + 1; }
       }
     }
+    // small ranges: exact SAH over every centroid-sorted split (the binned
+    // estimate is coarse when a node holds a few dozen triangles)
+    bool exact = false;
+    std::vector<uint32_t> exact_order;
+    if (count <= opt.exact_sah_below) {
+      std::vector<uint32_t> idx(order.begin() + first, order.begin() + first + count);
+      std::vector<float> racc(count);
+      for (int axis = 0; axis < 3; ++axis) {
+        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+          return centroid[3 * a + axis] < centroid[3 * b + axis];
+        });
+        Box acc;
+        for (uint32_t k = count; k-- > 1;) { acc.grow(prim_box[idx[k]]); racc[k] = acc.area(); }
+        acc = Box();
+        for (uint32_t k = 0; k + 1 < count; ++k) {
+          acc.grow(prim_box[idx[k]]);
+          const float cost = acc.area() * (float)(k + 1) + racc[k + 1] * (float)(count - k - 1);
+          if (cost < best_cost) {
+            best_cost = cost;
+            best_axis = axis;
+            best_split = k + 1;
+            exact = true;
+            exact_order = idx;
+          }
+        }
+      }
+    }
     const float parent_area = box.area();
     const float split_cost = parent_area > 0.0f ? opt.traversal_cost + best_cost / parent_area : FLT_MAX;
     uint32_t mid;
-    if (best_axis < 0) {
+    if (exact) {
+      if (count <= opt.max_leaf_size && leaf_cost <= split_cost) { make_leaf(id, first, count, depth); return id; }
+      std::copy(exact_order.begin(), exact_order.end(), order.begin() + first);
+      mid = first + best_split;
+    } else if (best_axis < 0) {
       // all centroids coincide: leaf if it fits, else split the range in half
       if (count <= opt.max_leaf_size) { make_leaf(id, first, count, depth); return id; }
       mid = first + count / 2;

@@ -464,6 +464,8 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   // tuning overrides (profiling): MRT_LEAF = max leaf size, MRT_CTRAV = SAH node cost
   if (const char* v = std::getenv("MRT_LEAF")) opt.max_leaf_size = (uint32_t)std::strtoul(v, nullptr, 0);
   if (const char* v = std::getenv("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
+  if (const char* v = std::getenv("MRT_BINS")) opt.bins = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (const char* v = std::getenv("MRT_EXACT_SAH")) opt.exact_sah_below = (uint32_t)std::strtoul(v, nullptr, 0);
   opt.width = desc->bvh_width ? desc->bvh_width : 4;
   if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
   if (opt.width != 2 && opt.width != 4) return fail(MRT_ERR_INVALID, "bvh_width must be 2 or 4");
