@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="N=1 only: time rank 0's tiles of an S-way tile split (one GPU's share)")
+    p.add_argument("--shard-rank", type=int, default=0,
+                   help="with --shard-of: which rank's tiles to render (default 0)")
     p.add_argument("--exchange", default="gather", choices=["gather", "reduce"],
                    help="N>1 image exchange: RCCL gather of packed owned tiles (default) or SUM reduce of the image")
     p.add_argument("--check-image", action="store_true",
@@ -190,7 +192,8 @@ def main():
     # runtime copy, so streams are not shared: r.sync() orders the reduce)
     image = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
-    r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True, shard_rank=rank, shard_count=shard_count,
+    r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True,
+                     shard_rank=(args.shard_rank if args.shard_of else rank), shard_count=shard_count,
                      image_ptr=image.data_ptr())
     r.prepare(spp)
 
@@ -303,7 +306,7 @@ def main():
                 (f" + seeded procedural mesh ({cfg['procedural']} tris)" if cfg["procedural"] else "") +
                 ", deterministic noise seed",
         "config": {"workload": cfg["workload"], "width": W, "height": H, "spp": spp, "max_path_length": L,
-                   "scene": cfg["scene"], "parallelism": (f"tile shard 0 of {shard_count} (one GPU's share)" if args.shard_of else
+                   "scene": cfg["scene"], "parallelism": (f"tile shard {args.shard_rank} of {shard_count} (one GPU's share)" if args.shard_of else
                                    f"tiles64x{world}" + (f" + rccl {args.exchange}" if world > 1 else "")),
                    "build": "precise" if args.precise else "fast",
                    "bvh": {"builder": {"sah": "host-sah", "lbvh": "device-lbvh", "ploc": "device-ploc"}[args.bvh],

@@ -248,10 +248,17 @@ int mrt_tiles_unpack(const float* packed, uint32_t width, uint32_t height, uint3
 /* Wait for work queued by libmrt on `stream` (NULL = everything on the device
  * libmrt's runtime has queued). */
 int mrt_synchronize(void* stream);
-/* Diagnostics: cycles spent per phase of the bounce loop, summed over waves
- * (out[0..4] = load, trace, shade, shadow, finish; out[5] = wave iterations).
+/* Diagnostics: cycles spent per phase of the bounce loop, summed over the
+ * waves of the last launch of each bounce index % 4 (out[0..4] = load, trace, shade, shadow, finish; out[5] = wave iterations).
  * Non-zero only in the separately built stamp library (make stamps). */
 int mrt_debug_stamps(uint64_t* out8, int reset);
+/* Diagnostics: per-wave timeline of the last bounce launch of each bounce
+ * index % 4: out[((b % 4) * 8192 + wave) * 16 + k], k = {first iteration,
+ * exit, iterations | exit reason << 32 (1 input exhausted, 2 output segment
+ * full), last grab, end of the last grab's work, summed grab latency, max
+ * grab latency, last grab's latency, phase cycles 0..4} in 100 MHz real-time ticks; n = number
+ * of uint64 to copy (at most 4 * 8192 * 16).  Zeros outside the stamp library. */
+int mrt_debug_wave_times(uint64_t* out, size_t n);
 /* Number of HIP devices visible (0 when none; never fails). */
 int mrt_device_count(void);
 

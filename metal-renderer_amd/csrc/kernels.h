@@ -41,8 +41,12 @@ constexpr uint32_t kMaxBatch = 64;
 // kSegSlack >= (waves per block + 1) * kGrab keeps at least one block able to
 // grab until the input is exhausted (see bounce_kernel).
 constexpr uint32_t kGrab = 128;
-constexpr uint32_t kGrabRanges = 16;
-constexpr uint32_t kGrabStride = 32;    // uint32 words between counters
+constexpr uint32_t kGrabRanges = 16;   // <= 31: the probe's open mask is one 32-bit ballot word
+static_assert(kGrabRanges <= 31, "kGrabRanges");
+#ifndef MRT_GRAB_STRIDE
+#define MRT_GRAB_STRIDE 32
+#endif
+constexpr uint32_t kGrabStride = MRT_GRAB_STRIDE;    // uint32 words between counters
 constexpr uint32_t kSegSlack = 1024;
 
 struct BounceArgs {
@@ -122,6 +126,8 @@ struct AccumArgs {
                                uint32_t count, bool pack, hipStream_t s);                                 \
   /* diagnostic phase stamps (MRT_STAMPS builds; zeros otherwise) */                                      \
   hipError_t read_stamps(unsigned long long* out8, bool reset);                                          \
+  /* per-wave timeline {start, exit, iterations} of the last launch of each bounce % 4 (stamp builds) */   \
+  hipError_t read_wave_times(unsigned long long* out, size_t n);                                         \
   }
 
 MRT_DECLARE_LAUNCHERS(precise)

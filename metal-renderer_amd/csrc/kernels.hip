@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "kernels.h"
 
@@ -803,14 +804,14 @@ __device__ __forceinline__ void accumulate_pixel(float4* image, uint32_t pix, V3
 // ---------------------------------------------------------------------------
 // Diagnostic phase stamps (MRT_STAMPS builds only; never in the product):
 // s_memtime around each wave-uniform phase of the bounce loop, summed per
-// wave in SGPRs and added once per wave into g_stamps at kernel exit.  The
-// stamp waits for vmcnt/lgkmcnt(0), so read the SHARES, not the length.
+// wave in SGPRs and stored once per wave (plain stores into g_wave_t) at
+// exit, with the wave's launch timeline.  The stamp waits for
+// vmcnt/lgkmcnt(0), so read the SHARES, not the length.
 // ---------------------------------------------------------------------------
 #ifndef MRT_STAMPS
 #define MRT_STAMPS 0
 #endif
 #if MRT_STAMPS
-__device__ unsigned long long g_stamps[8];
 __device__ __forceinline__ uint64_t stamp_now() {
   uint64_t t;
   __builtin_amdgcn_sched_barrier(0);
@@ -818,17 +819,46 @@ __device__ __forceinline__ uint64_t stamp_now() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-#define STAMP_DECL() uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}; uint64_t st_prev = 0; uint64_t st_iters = 0
+// per-wave timeline of the last launch of each bounce index (b % 4), in
+// s_memrealtime ticks (100 MHz, chip-wide), wave id = block * 4 + wave:
+// {first iteration start, exit, iterations | exit reason << 32 (1 = input
+// exhausted, 2 = output segment full), last grab, end of the last grab's
+// work, summed grab latency, max grab latency, last grab's latency, phase
+// cycles 0..4 (s_memtime)} — plain stores, so the exit is not a storm of
+// atomics on a few words
+constexpr uint32_t kStampWaves = 8192;
+constexpr uint32_t kStampFields = 16;
+__device__ unsigned long long g_wave_t[4][kStampWaves][kStampFields];
+__device__ __forceinline__ uint64_t stamp_real() {
+  uint64_t t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define STAMP_DECL() uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0}; uint64_t st_prev = 0; uint64_t st_iters = 0; \
+    const uint64_t st_t0 = stamp_real(); uint64_t st_why = 0, st_grab = 0, st_work = 0, st_ab = 0, \
+    st_asum = 0, st_amax = 0
 #define STAMP_BEGIN() do { st_prev = stamp_now(); ++st_iters; } while (0)
 #define STAMP(k) do { const uint64_t t_ = stamp_now(); st_acc[k] += t_ - st_prev; st_prev = t_; } while (0)
 #define STAMP_FLUSH() do { if ((threadIdx.x & 63u) == 0) { \
-    for (int k_ = 0; k_ < 5; ++k_) atomicAdd(&g_stamps[k_], (unsigned long long)st_acc[k_]); \
-    atomicAdd(&g_stamps[5], (unsigned long long)st_iters); } } while (0)
+    const uint32_t w_ = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u; \
+    if (w_ < kStampWaves) { unsigned long long* e_ = g_wave_t[a.bounce & 3u][w_]; \
+      e_[0] = st_t0; e_[1] = stamp_real(); e_[2] = st_iters | (st_why << 32); e_[3] = st_grab; \
+      e_[4] = st_work; e_[5] = st_asum; e_[6] = st_amax; e_[7] = st_grab - st_ab; \
+      for (int k_ = 0; k_ < 5; ++k_) e_[8 + k_] = st_acc[k_]; } } } while (0)
+#define STAMP_ATOMIC_BEGIN() do { st_ab = stamp_real(); } while (0)
+#define STAMP_EXIT(got) do { st_why = (got) == 0xFFFFFFFEu ? 2u : 1u; } while (0)
+#define STAMP_GRAB() do { st_grab = stamp_real(); st_asum += st_grab - st_ab; \
+    st_amax = st_grab - st_ab > st_amax ? st_grab - st_ab : st_amax; } while (0)
+#define STAMP_WORK() do { st_work = stamp_real(); } while (0)
 #else
 #define STAMP_DECL() do {} while (0)
 #define STAMP_BEGIN() do {} while (0)
 #define STAMP(k) do {} while (0)
 #define STAMP_FLUSH() do {} while (0)
+#define STAMP_EXIT(got) do {} while (0)
+#define STAMP_GRAB() do {} while (0)
+#define STAMP_WORK() do {} while (0)
+#define STAMP_ATOMIC_BEGIN() do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -881,13 +911,13 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n
 template <int STACK, int MODE, int WIDTH>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
-  __shared__ uint32_t s_cursor[2], s_res;
+  __shared__ uint32_t s_cursor[2], s_res, s_closed;
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
   const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1, a.stack_spill);
   uint32_t* seg = lds_u32() + cx.scratch_base;   // exclusive prefix of the input segments
-  if (tid == 0) s_cursor[0] = s_cursor[1] = s_res = 0;
+  if (tid == 0) s_cursor[0] = s_cursor[1] = s_res = s_closed = 0;
 
   uint32_t N, in_chunk = 0;
   if (a.bounce == 0) {
@@ -928,22 +958,35 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     uint32_t start, end, niter;
     if (dynamic) {
       uint32_t got = 0xFFFFFFFFu;
-      if (lane == 0 && atomicAdd(&s_res, kGrab) + kGrab <= cap) {
-        while (ranges_left) {
-          const uint32_t r0 = cur_range * rlen;
-          if (r0 < N) {
-            const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
-            if (i < rlen && r0 + i < N) { got = r0 + i; break; }
+      STAMP_ATOMIC_BEGIN();
+      if (lane == 0) {
+        if (atomicAdd(&s_res, kGrab) + kGrab <= cap) {
+          // s_closed: ranges a wave of this block found exhausted, so the
+          // block's other waves skip them without a device atomic (walking
+          // the exhausted ranges one atomic at a time delayed the launch's
+          // last exits by ~30 us: C2 +1.6 %, one GPU's 1/8 share +3.5 %;
+          // publishing closed ranges in a launch-wide mask word measured
+          // slower than the per-block mask alone)
+          while (ranges_left) {
+            const uint32_t r0 = cur_range * rlen;
+            if (r0 < N && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
+              const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
+              if (i < rlen && r0 + i < N) { got = r0 + i; break; }
+              atomicOr(&s_closed, 1u << cur_range);
+            }
+            cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
+            --ranges_left;
           }
-          cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
-          --ranges_left;
+          if (got == 0xFFFFFFFFu) atomicSub(&s_res, kGrab);   // input exhausted
+        } else {
+          got = 0xFFFFFFFEu;                                   // block's output segment full
         }
-        if (got == 0xFFFFFFFFu) atomicSub(&s_res, kGrab);
       }
       got = __builtin_amdgcn_readfirstlane(got);
-      if (got == 0xFFFFFFFFu) break;
+      if (got >= 0xFFFFFFFEu) { STAMP_EXIT(got); break; }
       cur_range = __builtin_amdgcn_readfirstlane(cur_range);
       ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
+      STAMP_GRAB();
       start = got;
       end = min(N, cur_range * rlen + rlen);
       niter = kGrab / 64;
@@ -1075,6 +1118,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     if (alive && !(a.debug & 4u)) a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
     STAMP(4);
     }
+    STAMP_WORK();
     if (dynamic && lane == 0) atomicSub(&s_res, kGrab - wrote);
   }
   STAMP_FLUSH();
@@ -1452,15 +1496,35 @@ hipError_t launch_tiles_move(const float4* src, float4* dst, uint32_t W, uint32_
   return hipGetLastError();
 }
 
-hipError_t read_stamps(unsigned long long* out8, bool reset) {
+hipError_t read_wave_times(unsigned long long* out, size_t n) {
 #if MRT_STAMPS
-  hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), 8 * sizeof(unsigned long long));
-  if (e != hipSuccess || !reset) return e;
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), std::min(n, (size_t)4 * kStampWaves * kStampFields) * sizeof(unsigned long long));
+#else
+  for (size_t k = 0; k < n; ++k) out[k] = 0;
+  return hipSuccess;
+#endif
+}
+
+hipError_t read_stamps(unsigned long long* out8, bool reset) {
+  for (int k = 0; k < 8; ++k) out8[k] = 0;
+#if MRT_STAMPS
+  // phase cycles and iterations summed over the per-wave records of the last
+  // launch of each bounce index
+  std::vector<unsigned long long> w((size_t)4 * kStampWaves * kStampFields);
+  hipError_t e = hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_wave_t), w.size() * sizeof(unsigned long long));
+  if (e != hipSuccess) return e;
+  for (size_t i = 0; i < (size_t)4 * kStampWaves; ++i) {
+    const unsigned long long* r = &w[i * kStampFields];
+    for (int k = 0; k < 5; ++k) out8[k] += r[8 + k];
+    out8[5] += r[2] & 0xFFFFFFFFull;
+  }
+  if (reset) {
+    std::fill(w.begin(), w.end(), 0ull);
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_wave_t), w.data(), w.size() * sizeof(unsigned long long));
+  }
+  return e;
 #else
   (void)reset;
-  for (int k = 0; k < 8; ++k) out8[k] = 0;
   return hipSuccess;
 #endif
 }

@@ -433,6 +433,12 @@ int mrt_debug_stamps(uint64_t* out8, int reset) {
   return MRT_OK;
 }
 
+int mrt_debug_wave_times(uint64_t* out, size_t n) {
+  if (!out) return fail(MRT_ERR_INVALID, "null output");
+  HIP_TRY(mrt::fast::read_wave_times(reinterpret_cast<unsigned long long*>(out), n));
+  return MRT_OK;
+}
+
 int mrt_noise_table(uint64_t seed, int64_t frame, float* out) {
   if (!out) return fail(MRT_ERR_INVALID, "null output");
   mrt::make_noise_table(seed, frame, out);

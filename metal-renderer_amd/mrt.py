@@ -120,7 +120,7 @@ EXPORTED = [
     "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image",
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
-    "mrt_debug_stamps", "mrt_shard_mask",
+    "mrt_debug_stamps", "mrt_debug_wave_times", "mrt_shard_mask",
     "mrt_tiles_packed_floats", "mrt_tiles_pack", "mrt_tiles_unpack", "mrt_display", "mrt_renderer_set_max_frames",
     "mrt_accel_create", "mrt_accel_rebuild", "mrt_accel_intersect", "mrt_accel_info_get", "mrt_accel_destroy",
 ]
@@ -170,6 +170,7 @@ def lib() -> ctypes.CDLL:
         "mrt_device_count": [],
         "mrt_synchronize": [vp],
         "mrt_debug_stamps": [vp, c_int],
+        "mrt_debug_wave_times": [vp, ctypes.c_size_t],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
         "mrt_tiles_packed_floats": [u32, u32, u32, u32, ctypes.POINTER(u64)],
         "mrt_display": [vp, vp, vp, u32, u32, u32, ctypes.c_float, vp],
@@ -500,6 +501,18 @@ def debug_stamps(reset: bool = True):
     import numpy as np
     out = np.zeros(8, np.uint64)
     _check(lib().mrt_debug_stamps(ctypes.c_void_p(out.ctypes.data), int(reset)), "mrt_debug_stamps")
+    return out
+
+
+def debug_wave_times():
+    """Per-wave timeline of the last launch of each bounce index % 4 (stamp
+    library only), shape (4, 8192, 16), 100 MHz ticks: {start, exit,
+    iterations | exit reason << 32, last grab, end of the last grab's work,
+    summed grab latency, max grab latency, last grab's latency, phase
+    cycles 0..4, 0, 0, 0}."""
+    import numpy as np
+    out = np.zeros((4, 8192, 16), np.uint64)
+    _check(lib().mrt_debug_wave_times(ctypes.c_void_p(out.ctypes.data), out.size), "mrt_debug_wave_times")
     return out
 
 
