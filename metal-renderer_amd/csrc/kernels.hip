@@ -788,17 +788,17 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
   }
 }
 
-// accumulateImage — renderer/Shaders.metal:233-249
-__device__ __forceinline__ void accumulate_pixel(float4* image, uint32_t pix, V3 c, uint32_t f) {
-  float4 out;
+// accumulateImage — renderer/Shaders.metal:233-249: the value written for
+// frame f given the stored pixel
+__device__ __forceinline__ float4 accumulate_value(const float4& stored, V3 c, uint32_t f) {
   if (f > 0) {
     const float factor = m_div(float(f), float(f + 1));
-    const float4 stored = image[pix];
-    out = make_float4(mixf(c.x, stored.x, factor), mixf(c.y, stored.y, factor), mixf(c.z, stored.z, factor), 1.0f);
-  } else {
-    out = make_float4(c.x, c.y, c.z, 1.0f);
+    return make_float4(mixf(c.x, stored.x, factor), mixf(c.y, stored.y, factor), mixf(c.z, stored.z, factor), 1.0f);
   }
-  image[pix] = out;
+  return make_float4(c.x, c.y, c.z, 1.0f);
+}
+__device__ __forceinline__ void accumulate_pixel(float4* image, uint32_t pix, V3 c, uint32_t f) {
+  image[pix] = accumulate_value(f > 0 ? image[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f), c, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -824,7 +824,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
 // {first iteration start, exit, iterations | exit reason << 32 (1 = input
 // exhausted, 2 = output segment full), last grab, end of the last grab's
 // work, summed grab latency, max grab latency, last grab's latency, phase
-// cycles 0..4 (s_memtime)} — plain stores, so the exit is not a storm of
+// cycles 0..4 (s_memtime), kernel entry (before the LDS staging)} — plain stores, so the exit is not a storm of
 // atomics on a few words
 constexpr uint32_t kStampWaves = 8192;
 constexpr uint32_t kStampFields = 16;
@@ -844,7 +844,8 @@ __device__ __forceinline__ uint64_t stamp_real() {
     if (w_ < kStampWaves) { unsigned long long* e_ = g_wave_t[a.bounce & 3u][w_]; \
       e_[0] = st_t0; e_[1] = stamp_real(); e_[2] = st_iters | (st_why << 32); e_[3] = st_grab; \
       e_[4] = st_work; e_[5] = st_asum; e_[6] = st_amax; e_[7] = st_grab - st_ab; \
-      for (int k_ = 0; k_ < 5; ++k_) e_[8 + k_] = st_acc[k_]; } } } while (0)
+      for (int k_ = 0; k_ < 5; ++k_) e_[8 + k_] = st_acc[k_]; e_[13] = st_entry; } } } while (0)
+#define STAMP_ENTRY() const uint64_t st_entry = stamp_real()
 #define STAMP_ATOMIC_BEGIN() do { st_ab = stamp_real(); } while (0)
 #define STAMP_EXIT(got) do { st_why = (got) == 0xFFFFFFFEu ? 2u : 1u; } while (0)
 #define STAMP_GRAB() do { st_grab = stamp_real(); st_asum += st_grab - st_ab; \
@@ -859,6 +860,7 @@ __device__ __forceinline__ uint64_t stamp_real() {
 #define STAMP_GRAB() do {} while (0)
 #define STAMP_WORK() do {} while (0)
 #define STAMP_ATOMIC_BEGIN() do {} while (0)
+#define STAMP_ENTRY() do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -912,6 +914,7 @@ template <int STACK, int MODE, int WIDTH>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
   __shared__ uint32_t s_cursor[2], s_res, s_closed;
+  STAMP_ENTRY();
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
@@ -1142,10 +1145,25 @@ __global__ __launch_bounds__(kBlock) void accumulate_frame_kernel(AccumArgs a) {
     slot_pixel(idx, a.shard_rank, a.shard_count, a.tiles_x, x, y);
     if (x >= a.width || y >= a.height) continue;
     const uint32_t pix = y * a.width + x;
-    for (uint32_t j = 0; j < a.batch; ++j) {
-      const float4 c = a.radiance[j * a.num_slots + idx];
-      accumulate_pixel(a.image, pix, mk(c), a.frame_index + j);
+    // the running mean stays in registers across the batch's frames (one
+    // image read and one write per pixel); radiance rows are read once,
+    // eight frames' loads in flight at a time
+    float4 cur = a.frame_index > 0 ? a.image[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4* rad = a.radiance + idx;
+    uint32_t j = 0;
+    for (; j + 8 <= a.batch; j += 8) {
+      float4 c[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(rad + (size_t)(j + k) * a.num_slots));
+        c[k] = make_float4(v.x, v.y, v.z, v.w);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cur = accumulate_value(cur, mk(c[k]), a.frame_index + j + k);
     }
+    for (; j < a.batch; ++j) cur = accumulate_value(cur, mk(rad[(size_t)j * a.num_slots]), a.frame_index + j);
+    a.image[pix] = cur;
   }
 }
 
