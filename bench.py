@@ -208,9 +208,15 @@ def main():
         gathered = [torch.zeros(packed_n, dtype=torch.float32, device=tdev) for _ in range(world)] if rank == 0 else None
         torch.cuda.synchronize()
 
+    rstream = r.stream()
+
     def exchange():
-        r.sync()
         torch.cuda.synchronize()   # the previous step's collective has released `packed` / `image`
+        if args.exchange == "gather":
+            # packed on the renderer's stream right behind the draw: one host
+            # wait (r.sync) covers the draw and the pack
+            mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed.data_ptr(), stream=rstream, sync=False)
+        r.sync()
         if args.exchange == "reduce":
             if args.dist_backend == "nccl":
                 dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
@@ -221,7 +227,6 @@ def main():
                     image.copy_(host.cuda())
                     torch.cuda.synchronize()
             return
-        mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed.data_ptr())   # libmrt runtime, synchronised
         src = packed if args.dist_backend == "nccl" else packed.cpu()
         dist.gather(src, gathered, dst=0)   # the single RCCL gather of the packed tiles (xGMI)
         if rank == 0:

@@ -200,6 +200,10 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n);
 int mrt_renderer_sync(mrt_renderer* r);
 /* Device pointer of the accumulation image (for an RCCL reduce). */
 int mrt_renderer_image(mrt_renderer* r, float** device_image);
+/* The renderer's main HIP stream (libmrt's runtime): work queued on it, e.g.
+ * mrt_tiles_pack of the image, runs after the renderer's draws without a
+ * host round trip. */
+int mrt_renderer_stream(mrt_renderer* r, void** stream);
 /* Synchronise and copy the image to host memory (rgba must hold W*H*4 floats). */
 int mrt_renderer_read_image(mrt_renderer* r, float* rgba, size_t count);
 /* MAX_FRAMES (Raytracing.h:28, Renderer.mm:589-590): once frame_index reaches

@@ -1083,6 +1083,12 @@ int mrt_renderer_image(mrt_renderer* r, float** device_image) {
   return MRT_OK;
 }
 
+int mrt_renderer_stream(mrt_renderer* r, void** stream) {
+  if (!r || !stream) return fail(MRT_ERR_INVALID, "null argument");
+  *stream = (void*)r->stream;
+  return MRT_OK;
+}
+
 int mrt_renderer_read_image(mrt_renderer* r, float* rgba, size_t count) {
   if (!r || !rgba) return fail(MRT_ERR_INVALID, "null argument");
   const size_t need = (size_t)r->desc.width * r->desc.height * 4;

@@ -117,7 +117,7 @@ EXPORTED = [
     "mrt_scene_create", "mrt_scene_info_get", "mrt_scene_export", "mrt_scene_destroy", "mrt_scene_check_bvh",
     "mrt_raygen", "mrt_intersect", "mrt_shade", "mrt_resolve_shadow", "mrt_accumulate",
     "mrt_renderer_create", "mrt_renderer_resize", "mrt_renderer_reset", "mrt_renderer_prepare",
-    "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image",
+    "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image", "mrt_renderer_stream",
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
     "mrt_debug_stamps", "mrt_debug_wave_times", "mrt_shard_mask",
@@ -160,6 +160,7 @@ def lib() -> ctypes.CDLL:
         "mrt_renderer_draw_n": [vp, u32],
         "mrt_renderer_sync": [vp],
         "mrt_renderer_image": [vp, ctypes.POINTER(vp)],
+        "mrt_renderer_stream": [vp, ctypes.POINTER(vp)],
         "mrt_renderer_read_image": [vp, vp, ctypes.c_size_t],
         "mrt_renderer_save_image": [vp, ctypes.c_char_p],
         "mrt_renderer_stats": [vp, ctypes.POINTER(Stats)],
@@ -340,6 +341,12 @@ class Renderer:
     def image_ptr(self) -> int:
         p = ctypes.c_void_p()
         _check(lib().mrt_renderer_image(self._h, ctypes.byref(p)), "mrt_renderer_image")
+        return p.value
+
+    def stream(self) -> int:
+        """The renderer's main stream (libmrt's HIP runtime)."""
+        p = ctypes.c_void_p()
+        _check(lib().mrt_renderer_stream(self._h, ctypes.byref(p)), "mrt_renderer_stream")
         return p.value
 
     def read_image(self):
