@@ -74,6 +74,8 @@ def parse():
                    help="with --shard-of: which rank's tiles to render (default 0)")
     p.add_argument("--exchange", default="gather", choices=["gather", "reduce"],
                    help="N>1 image exchange: RCCL gather of packed owned tiles (default) or SUM reduce of the image")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="N > 1: exchange inside each step instead of overlapping it with the next step's draw")
     p.add_argument("--check-image", action="store_true",
                    help="N>1: rank 0 renders the frame alone afterwards and asserts the exchanged image is bitwise equal")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -202,47 +204,82 @@ def main():
     # (1/N of the image per rank), or one RCCL SUM reduce of the whole image
     # (non-owned pixels are 0); both give the 1-GPU image bitwise
     packed_n = mrt.tiles_packed_floats(W, H, 0, world) if world > 1 else 0   # rank 0 owns the most tiles
+    # --overlap (default for the gather): step k's tiles are packed on the
+    # renderer's stream behind its draw and gathered during step k+1's draw
+    # (double-buffered packed tiles; rank 0 unpacks on the renderer's stream,
+    # non-owned tiles only, so it never touches the pixels being rendered);
+    # the last step's exchange is flushed inside the timed region
+    overlap = world > 1 and args.exchange == "gather" and not args.no_overlap
+    nccl = args.dist_backend == "nccl"
+    rstream = r.stream()
     if world > 1:
-        tdev = "cuda" if args.dist_backend == "nccl" else "cpu"
-        packed = torch.zeros(packed_n, dtype=torch.float32, device="cuda")
+        tdev = "cuda" if nccl else "cpu"
+        packed = [torch.zeros(packed_n, dtype=torch.float32, device="cuda") for _ in range(2 if overlap else 1)]
+        pack_done = [mrt.Event() for _ in packed]
         gathered = [torch.zeros(packed_n, dtype=torch.float32, device=tdev) for _ in range(world)] if rank == 0 else None
         torch.cuda.synchronize()
 
-    rstream = r.stream()
+    def gather_unpack(i):
+        """The single RCCL gather (xGMI) of buffer i's packed tiles to rank 0,
+        which unpacks them into the image on the renderer's stream."""
+        pack_done[i].synchronize()   # host wait: libmrt's pack of buffer i is complete
+        src = packed[i] if nccl else packed[i].cpu()
+        dist.gather(src, gathered, dst=0)
+        if rank == 0:
+            bufs = gathered if nccl else [g.cuda() for g in gathered]
+            torch.cuda.synchronize()   # the gather (and copies) in torch's runtime are complete
+            for k in range(1, world):
+                mrt.tiles_unpack(bufs[k].data_ptr(), W, H, k, world, image.data_ptr(), stream=rstream, sync=False)
+            if not nccl:
+                r.sync()   # the temporary device copies are released on return
 
     def exchange():
+        """One exchange inside the step (--no-overlap, or --exchange reduce)."""
         torch.cuda.synchronize()   # the previous step's collective has released `packed` / `image`
-        if args.exchange == "gather":
-            # packed on the renderer's stream right behind the draw: one host
-            # wait (r.sync) covers the draw and the pack
-            mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed.data_ptr(), stream=rstream, sync=False)
-        r.sync()
         if args.exchange == "reduce":
-            if args.dist_backend == "nccl":
+            r.sync()
+            if nccl:
                 dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
             else:
                 host = image.cpu()
                 dist.reduce(host, dst=0)
                 if rank == 0:
                     image.copy_(host.cuda())
-                    torch.cuda.synchronize()
-            return
-        src = packed if args.dist_backend == "nccl" else packed.cpu()
-        dist.gather(src, gathered, dst=0)   # the single RCCL gather of the packed tiles (xGMI)
-        if rank == 0:
             torch.cuda.synchronize()
-            for k in range(1, world):
-                g = gathered[k] if args.dist_backend == "nccl" else gathered[k].cuda()
-                mrt.tiles_unpack(g.data_ptr(), W, H, k, world, image.data_ptr(), sync=(k == world - 1))
+            return
+        mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed[0].data_ptr(), stream=rstream, sync=False)
+        pack_done[0].record(rstream)
+        gather_unpack(0)
+        r.sync()
+
+    state = {"k": 0, "pending": None}
 
     def step():
         r.reset()
         r.draw(spp)
-        if world > 1:
+        if world == 1:
+            return
+        if not overlap:
             exchange()
+            return
+        i = state["k"] % 2
+        torch.cuda.synchronize()   # the gather that read packed[i] two steps ago has completed
+        if state["pending"] is not None:
+            gather_unpack(state["pending"])   # the previous step's tiles move while this step renders
+        mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed[i].data_ptr(), stream=rstream, sync=False)
+        pack_done[i].record(rstream)
+        state["pending"] = i
+        state["k"] += 1
+
+    def flush():
+        if overlap and state["pending"] is not None:
+            torch.cuda.synchronize()
+            gather_unpack(state["pending"])
+            state["pending"] = None
 
     for _ in range(args.warmup):
         step()
+    flush()
     r.sync()
     torch.cuda.synchronize()
     base = r.stats()
@@ -252,6 +289,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    flush()
     r.sync()
     torch.cuda.synchronize()
     if world > 1:

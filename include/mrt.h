@@ -252,6 +252,13 @@ int mrt_tiles_unpack(const float* packed, uint32_t width, uint32_t height, uint3
 /* Wait for work queued by libmrt on `stream` (NULL = everything on the device
  * libmrt's runtime has queued). */
 int mrt_synchronize(void* stream);
+/* Stream-ordered completion markers in libmrt's runtime (the host-side
+ * ordering between libmrt's work and another runtime's, e.g. the multi-GPU
+ * exchange): record an event on `stream` (NULL = the default stream),
+ * creating it first when *event is NULL; wait for it; destroy it. */
+int mrt_event_record(void* stream, void** event);
+int mrt_event_synchronize(void* event);
+int mrt_event_destroy(void* event);
 /* Diagnostics: cycles spent per phase of the bounce loop, summed over the
  * waves of the last launch of each bounce index % 4 (out[0..4] = load, trace, shade, shadow, finish; out[5] = wave iterations).
  * Non-zero only in the separately built stamp library (make stamps). */

@@ -427,6 +427,28 @@ int mrt_synchronize(void* stream) {
   return MRT_OK;
 }
 
+int mrt_event_record(void* stream, void** event) {
+  if (!event) return fail(MRT_ERR_INVALID, "null event");
+  if (!*event) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *event = (void*)e;
+  }
+  HIP_TRY(hipEventRecord((hipEvent_t)*event, (hipStream_t)stream));
+  return MRT_OK;
+}
+
+int mrt_event_synchronize(void* event) {
+  if (!event) return fail(MRT_ERR_INVALID, "null event");
+  HIP_TRY(hipEventSynchronize((hipEvent_t)event));
+  return MRT_OK;
+}
+
+int mrt_event_destroy(void* event) {
+  if (event) HIP_TRY(hipEventDestroy((hipEvent_t)event));
+  return MRT_OK;
+}
+
 int mrt_debug_stamps(uint64_t* out8, int reset) {
   if (!out8) return fail(MRT_ERR_INVALID, "null output");
   HIP_TRY(mrt::fast::read_stamps(reinterpret_cast<unsigned long long*>(out8), reset != 0));

@@ -120,6 +120,7 @@ EXPORTED = [
     "mrt_renderer_draw", "mrt_renderer_draw_n", "mrt_renderer_sync", "mrt_renderer_image", "mrt_renderer_stream",
     "mrt_renderer_read_image", "mrt_renderer_save_image", "mrt_renderer_stats", "mrt_renderer_destroy",
     "mrt_last_error", "mrt_abi_version", "mrt_noise_table", "mrt_device_count", "mrt_synchronize",
+    "mrt_event_record", "mrt_event_synchronize", "mrt_event_destroy",
     "mrt_debug_stamps", "mrt_debug_wave_times", "mrt_shard_mask",
     "mrt_tiles_packed_floats", "mrt_tiles_pack", "mrt_tiles_unpack", "mrt_display", "mrt_renderer_set_max_frames",
     "mrt_accel_create", "mrt_accel_rebuild", "mrt_accel_intersect", "mrt_accel_info_get", "mrt_accel_destroy",
@@ -170,6 +171,9 @@ def lib() -> ctypes.CDLL:
         "mrt_noise_table": [u64, i64, vp],
         "mrt_device_count": [],
         "mrt_synchronize": [vp],
+        "mrt_event_record": [vp, ctypes.POINTER(vp)],
+        "mrt_event_synchronize": [vp],
+        "mrt_event_destroy": [vp],
         "mrt_debug_stamps": [vp, c_int],
         "mrt_debug_wave_times": [vp, ctypes.c_size_t],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
@@ -521,6 +525,25 @@ def debug_wave_times():
     out = np.zeros((4, 8192, 16), np.uint64)
     _check(lib().mrt_debug_wave_times(ctypes.c_void_p(out.ctypes.data), out.size), "mrt_debug_wave_times")
     return out
+
+
+class Event:
+    """A completion marker on a libmrt stream (host-side ordering against
+    another runtime's work, e.g. torch/RCCL in the multi-GPU exchange)."""
+
+    def __init__(self):
+        self._e = ctypes.c_void_p()
+
+    def record(self, stream=None) -> None:
+        _check(lib().mrt_event_record(stream, ctypes.byref(self._e)), "mrt_event_record")
+
+    def synchronize(self) -> None:
+        _check(lib().mrt_event_synchronize(self._e), "mrt_event_synchronize")
+
+    def close(self) -> None:
+        if self._e.value:
+            _check(lib().mrt_event_destroy(self._e), "mrt_event_destroy")
+            self._e = ctypes.c_void_p()
 
 
 def device_count() -> int:
