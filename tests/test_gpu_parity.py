@@ -290,3 +290,27 @@ def test_max_frames(gpu, mrt_mod):
     c = r2.read_image()
     r2.close()
     assert st["frame_index"] == 3 and a.tobytes() == b.tobytes() == c.tobytes()
+
+
+def test_pack_on_renderer_stream(gpu, mrt_mod):
+    """The overlapped exchange's pattern (bench.py): a shard renderer's owned
+    tiles packed on the renderer's stream behind its draw, completion observed
+    through a libmrt event, equal to the packed tiles of the synchronised image."""
+    W, H, count = 200, 130, 3
+    scene = _scene(mrt_mod, "cornellbox")
+    d_img = to_dev(np.zeros((H, W, 4), np.float32))
+    r = mrt_mod.Renderer(scene, W, H, 2, shard_rank=1, shard_count=count, image_ptr=dev_ptr(d_img))
+    n = mrt_mod.tiles_packed_floats(W, H, 1, count)
+    d_p = to_dev(np.zeros(n, np.float32))
+    ev = mrt_mod.Event()
+    r.draw(3)
+    mrt_mod.tiles_pack(dev_ptr(d_img), W, H, 1, count, dev_ptr(d_p), stream=r.stream(), sync=False)
+    ev.record(r.stream())
+    ev.synchronize()
+    got = from_dev(d_p, np.float32)
+    r.sync()
+    img = from_dev(d_img, np.float32).reshape(H, W, 4)
+    ev.close()
+    r.close()
+    assert np.any(img != 0)
+    assert got.tobytes() == mrt_mod.tiles_pack_host(img, 1, count).tobytes()
