@@ -1288,11 +1288,15 @@ size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_
 }
 
 // kTopLds: stage only as many top BVH nodes as keep the block's LDS within
-// 1/6 of the CU less a 2-KB margin for allocation granularity (the VGPR
-// budget allows 6 resident blocks of 4 waves); the BFS order makes any prefix
-// the top levels.  Full occupancy beats more staged nodes: C4 with 80 nodes
-// 828, ~100 nodes (at the edge) 780, 128 nodes 715 Mpaths/s.
-constexpr size_t kLdsPerBlockTarget = 160 * 1024 / 6 - 2048;
+// 1/MRT_BOUNCE_WAVES of the CU less a 2-KB margin for allocation granularity
+// (the VGPR budget allows MRT_BOUNCE_WAVES resident blocks of 4 waves); the
+// BFS order makes any prefix the top levels.  Full occupancy beats more
+// staged nodes (at 6 blocks/CU: C4 with 80 nodes 828, ~100 nodes (at the
+// edge) 780, 128 nodes 715 Mpaths/s).
+#ifndef MRT_LDS_BLOCKS
+#define MRT_LDS_BLOCKS MRT_BOUNCE_WAVES
+#endif
+constexpr size_t kLdsPerBlockTarget = 160 * 1024 / MRT_LDS_BLOCKS - 2048;
 DeviceScene fit_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
   if (mode != kTopLds) return sc;
   DeviceScene f = sc;
