@@ -119,11 +119,27 @@ struct Hit {
   bool found;
 };
 
+// MRT_NODE_PERM: in the all-in-LDS mode every BVH4 node's x and y plane rows
+// are staged in four copies, one per sign quadrant of (dir.x, dir.y), each
+// pre-ordered (near, far) for rays of that quadrant; a ray reads the copy of
+// its quadrant, so the box test pairs only the z planes by min/max (16 fewer
+// VALU ops per node).  Slab distances are monotone in the plane coordinate
+// for a fixed direction (in both builds), so the quadrant's near plane is
+// exactly the min of the pair and results are bit-identical.  (Eight octant
+// copies measured -7.5 % on C2: the larger LDS image cost a resident block.)
+#ifndef MRT_NODE_PERM
+#define MRT_NODE_PERM 1
+#endif
+constexpr uint32_t kQuadCopies = 4;                      // (x, y) sign quadrants
+constexpr uint32_t kQuadCopyF4 = 7;                      // six plane rows + the refs row
+constexpr uint32_t kQuadNodeF4 = kQuadCopies * kQuadCopyF4;
+
 struct RayBox {   // precomputed slab-test terms
   V3 inv;
 #if !MRT_PRECISE
   V3 oinv;
 #endif
+  uint32_t quad_f4;   // kQuadCopyF4 x quadrant; quadrant bit a set where direction component a (x, y) is negative
 };
 
 __device__ __forceinline__ float safe_inv(float d) {
@@ -137,6 +153,7 @@ __device__ __forceinline__ RayBox make_raybox(V3 o, V3 d) {
 #if !MRT_PRECISE
   r.oinv = mk(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
 #endif
+  r.quad_f4 = kQuadCopyF4 * ((fbits(r.inv.x) >> 31) | ((fbits(r.inv.y) >> 31) << 1));
   return r;
 }
 
@@ -180,7 +197,9 @@ __device__ __forceinline__ void box2(const float4& a, const float4& b, const flo
 
 // Box test of the four children of a BVH4 node (component-major node, see
 // mrt_layout.h); returns each child's entry distance, +inf for a miss or an
-// empty slot.
+// empty slot.  ORDERED: the x and y plane rows arrive as (near, far) (a
+// quadrant copy, see MRT_NODE_PERM); otherwise as (lo, hi).
+template <bool ORDERED>
 __device__ __forceinline__ void box4(const float4* q, V3 o, const RayBox& rb, float tmin, float tmax, float tn[4]) {
 #if MRT_PRECISE
   const float ox = o.x, oy = o.y, oz = o.z;
@@ -196,8 +215,14 @@ __device__ __forceinline__ void box4(const float4* q, V3 o, const RayBox& rb, fl
     const float x0 = slab(f[k], ox, rb.inv.x, oix), x1 = slab(f[4 + k], ox, rb.inv.x, oix);
     const float y0 = slab(f[8 + k], oy, rb.inv.y, oiy), y1 = slab(f[12 + k], oy, rb.inv.y, oiy);
     const float z0 = slab(f[16 + k], oz, rb.inv.z, oiz), z1 = slab(f[20 + k], oz, rb.inv.z, oiz);
-    const float tnear = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));
-    const float tfar = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
+    float tnear, tfar;
+    if constexpr (ORDERED) {
+      tnear = fmaxf(fmaxf(x0, y0), fmaxf(fminf(z0, z1), tmin));
+      tfar = fminf(fminf(x1, y1), fminf(fmaxf(z0, z1), tmax));
+    } else {
+      tnear = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));
+      tfar = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
+    }
     const bool live = (int32_t)fbits(f[24 + k]) != kEmptyChild;
     tn[k] = (live & (tnear <= tfar)) ? tnear : __builtin_inff();
   }
@@ -233,18 +258,30 @@ struct LdsCtx {
 
 __device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
 
+// float4s per staged node: MRT_NODE_PERM (all-in-LDS BVH4 only) stages four
+// quadrant copies of the six plane rows and the refs row (consecutive copies
+// start 28 banks apart, so lanes of different quadrants reading the same node
+// row hit disjoint banks)
+__host__ __device__ constexpr uint32_t node_stride_f4(int mode, uint32_t node_f4) {
+  return (MRT_NODE_PERM && mode == kAllLds && node_f4 == 8) ? kQuadNodeF4 : node_f4;
+}
+
 // float4 counts of the staged scene image for a mode
 // (node_f4 = float4s per node: 4 for BVH2, 8 for BVH4)
 __host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t node_f4, uint32_t nodes, uint32_t lds_nodes,
                                                       uint32_t tris, uint32_t mats, uint32_t lights) {
-  if (mode == kAllLds) return node_f4 * nodes + 3 * tris + 6 * tris + 2 * mats + 7 * lights;
+  if (mode == kAllLds) return node_stride_f4(mode, node_f4) * nodes + 3 * tris + 6 * tris + 2 * mats + 7 * lights;
   if (mode == kTopLds) return node_f4 * lds_nodes;
   return 0;
 }
 
 template <int MODE>
-__device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx& cx, int32_t node, float4* q) {
-  if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
+__device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx& cx, int32_t node, const RayBox& rb,
+                                            float4* q) {
+  if (MODE == kAllLds && MRT_NODE_PERM) {   // the ray's quadrant copy
+#pragma unroll
+    for (int i = 0; i < 7; ++i) q[i] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + i];
+  } else if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) q[i] = g_lds[8 * node + i];
   } else {
@@ -328,7 +365,9 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   const uint32_t M = (MODE == kAllLds) ? sc.num_materials : 0u;
   const uint32_t NL = (MODE == kAllLds) ? sc.num_lights + 1 : 0u;
   cx.n_lds_nodes = n_nodes;
-  cx.tri_base = nf4 * n_nodes;
+  const uint32_t node_f4 = node_stride_f4(MODE, nf4);
+  const bool copies = node_f4 != nf4;
+  cx.tri_base = node_f4 * n_nodes;
   cx.prim_base = cx.tri_base + 3 * T;
   cx.mat_base = cx.prim_base + 6 * T;
   cx.light_base = cx.mat_base + 2 * M;
@@ -343,8 +382,18 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
                             reinterpret_cast<const float4*>(sc.lights)};
     const uint32_t base[5] = {0u, cx.tri_base, cx.prim_base, cx.mat_base, cx.light_base};
     const uint32_t len[5] = {nf4 * n_nodes, 3 * T, 6 * T, 2 * M, 7 * NL};
-    for (int r = 0; r < 5; ++r)
+    for (int r = copies ? 1 : 0; r < 5; ++r)
       for (uint32_t i = threadIdx.x; i < len[r]; i += kBlock) g_lds[base[r] + i] = src[r][i];
+    if (copies) {   // quadrant copies: x, y rows (near, far), z rows (lo, hi), refs
+      for (uint32_t i = threadIdx.x; i < node_f4 * n_nodes; i += kBlock) {
+        const uint32_t node = i / node_f4, rem = i % node_f4;
+        const uint32_t quad = rem / kQuadCopyF4, row = rem % kQuadCopyF4;
+        const uint32_t axis = row >> 1;
+        const uint32_t flip = axis < 2 ? (quad >> axis) & 1u : 0u;
+        const uint32_t src_row = row < 6 ? 2 * axis + ((row & 1u) ^ flip) : 6u;
+        g_lds[i] = src[0][8 * node + src_row];
+      }
+    }
     __syncthreads();
   }
   return cx;
@@ -391,9 +440,9 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     return right_first ? rr : rl;
   } else {
     float4 q[7];
-    fetch_node4<MODE>(sc, cx, node, q);
+    fetch_node4<MODE>(sc, cx, node, rb, q);
     float t[4];
-    box4(q, o, rb, tmin, tmax, t);
+    box4<MODE == kAllLds && MRT_NODE_PERM>(q, o, rb, tmin, tmax, t);
     int32_t r[4] = {(int32_t)fbits(q[6].x), (int32_t)fbits(q[6].y), (int32_t)fbits(q[6].z), (int32_t)fbits(q[6].w)};
     const float inf = __builtin_inff();
     // near-to-far order for occlusion rays too: measured +2.5 % (C2) and
