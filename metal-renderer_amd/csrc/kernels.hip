@@ -130,6 +130,11 @@ struct Hit {
 #ifndef MRT_NODE_PERM
 #define MRT_NODE_PERM 1
 #endif
+// MRT_ROWSEL: the other modes (top nodes in LDS, the rest in global memory)
+// read a node's plane rows in ray order through per-lane row offsets.
+#ifndef MRT_ROWSEL
+#define MRT_ROWSEL 1
+#endif
 constexpr uint32_t kQuadCopies = 4;                      // (x, y) sign quadrants
 constexpr uint32_t kQuadCopyF4 = 7;                      // six plane rows + the refs row
 constexpr uint32_t kQuadNodeF4 = kQuadCopies * kQuadCopyF4;
@@ -199,7 +204,7 @@ __device__ __forceinline__ void box2(const float4& a, const float4& b, const flo
 // mrt_layout.h); returns each child's entry distance, +inf for a miss or an
 // empty slot.  ORDERED: the x and y plane rows arrive as (near, far) (a
 // quadrant copy, see MRT_NODE_PERM); otherwise as (lo, hi).
-template <bool ORDERED>
+template <int ORDERED>   // 0: (lo, hi) rows; 2: x, y rows (near, far); 3: all rows (near, far)
 __device__ __forceinline__ void box4(const float4* q, V3 o, const RayBox& rb, float tmin, float tmax, float tn[4]) {
 #if MRT_PRECISE
   const float ox = o.x, oy = o.y, oz = o.z;
@@ -216,7 +221,10 @@ __device__ __forceinline__ void box4(const float4* q, V3 o, const RayBox& rb, fl
     const float y0 = slab(f[8 + k], oy, rb.inv.y, oiy), y1 = slab(f[12 + k], oy, rb.inv.y, oiy);
     const float z0 = slab(f[16 + k], oz, rb.inv.z, oiz), z1 = slab(f[20 + k], oz, rb.inv.z, oiz);
     float tnear, tfar;
-    if constexpr (ORDERED) {
+    if constexpr (ORDERED == 3) {
+      tnear = fmaxf(fmaxf(x0, y0), fmaxf(z0, tmin));
+      tfar = fminf(fminf(x1, y1), fminf(z1, tmax));
+    } else if constexpr (ORDERED == 2) {
       tnear = fmaxf(fmaxf(x0, y0), fmaxf(fminf(z0, z1), tmin));
       tfar = fminf(fminf(x1, y1), fminf(fmaxf(z0, z1), tmax));
     } else {
@@ -281,13 +289,22 @@ __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx&
   if (MODE == kAllLds && MRT_NODE_PERM) {   // the ray's quadrant copy
 #pragma unroll
     for (int i = 0; i < 7; ++i) q[i] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + i];
-  } else if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) q[i] = g_lds[8 * node + i];
   } else {
-    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 8 * (size_t)node;
+    // MRT_ROWSEL (top-nodes mode): rows in ray order, (near, far) per axis by the direction's signs
+    const bool rowsel = MRT_ROWSEL && MODE == kTopLds;
+    const uint32_t sx = rowsel ? fbits(rb.inv.x) >> 31 : 0u, sy = rowsel ? fbits(rb.inv.y) >> 31 : 0u;
+    const uint32_t sz = rowsel ? fbits(rb.inv.z) >> 31 : 0u;
+    const uint32_t row[6] = {sx, 1u - sx, 2u + sy, 3u - sy, 4u + sz, 5u - sz};
+    if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
 #pragma unroll
-    for (int i = 0; i < 7; ++i) q[i] = p[i];
+      for (int i = 0; i < 6; ++i) q[i] = g_lds[8 * node + row[i]];
+      q[6] = g_lds[8 * node + 6];
+    } else {
+      const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 8 * (size_t)node;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) q[i] = p[row[i]];
+      q[6] = p[6];
+    }
   }
 }
 
@@ -442,7 +459,7 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     float4 q[7];
     fetch_node4<MODE>(sc, cx, node, rb, q);
     float t[4];
-    box4<MODE == kAllLds && MRT_NODE_PERM>(q, o, rb, tmin, tmax, t);
+    box4<(MODE == kAllLds && MRT_NODE_PERM) ? 2 : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0)>(q, o, rb, tmin, tmax, t);
     int32_t r[4] = {(int32_t)fbits(q[6].x), (int32_t)fbits(q[6].y), (int32_t)fbits(q[6].z), (int32_t)fbits(q[6].w)};
     const float inf = __builtin_inff();
     // near-to-far order for occlusion rays too: measured +2.5 % (C2) and
