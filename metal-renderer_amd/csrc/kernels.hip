@@ -135,6 +135,10 @@ struct Hit {
 #ifndef MRT_ROWSEL
 #define MRT_ROWSEL 1
 #endif
+// MRT_ZSEL: the quadrant copy's z rows are also read in ray order (row offsets)
+#ifndef MRT_ZSEL
+#define MRT_ZSEL 1
+#endif
 constexpr uint32_t kQuadCopies = 4;                      // (x, y) sign quadrants
 constexpr uint32_t kQuadCopyF4 = 7;                      // six plane rows + the refs row
 constexpr uint32_t kQuadNodeF4 = kQuadCopies * kQuadCopyF4;
@@ -287,8 +291,17 @@ template <int MODE>
 __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx& cx, int32_t node, const RayBox& rb,
                                             float4* q) {
   if (MODE == kAllLds && MRT_NODE_PERM) {   // the ray's quadrant copy
+#if MRT_ZSEL
+    const uint32_t sz = fbits(rb.inv.z) >> 31;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + i];
+    q[4] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + 4 + sz];
+    q[5] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + 5 - sz];
+    q[6] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + 6];
+#else
 #pragma unroll
     for (int i = 0; i < 7; ++i) q[i] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + i];
+#endif
   } else {
     // MRT_ROWSEL (top-nodes mode): rows in ray order, (near, far) per axis by the direction's signs
     const bool rowsel = MRT_ROWSEL && MODE == kTopLds;
@@ -459,7 +472,7 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     float4 q[7];
     fetch_node4<MODE>(sc, cx, node, rb, q);
     float t[4];
-    box4<(MODE == kAllLds && MRT_NODE_PERM) ? 2 : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0)>(q, o, rb, tmin, tmax, t);
+    box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0)>(q, o, rb, tmin, tmax, t);
     int32_t r[4] = {(int32_t)fbits(q[6].x), (int32_t)fbits(q[6].y), (int32_t)fbits(q[6].z), (int32_t)fbits(q[6].w)};
     const float inf = __builtin_inff();
     // near-to-far order for occlusion rays too: measured +2.5 % (C2) and
