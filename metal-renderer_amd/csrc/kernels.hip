@@ -122,8 +122,9 @@ struct Hit {
 // MRT_NODE_PERM: in the all-in-LDS mode every BVH4 node's x and y plane rows
 // are staged in four copies, one per sign quadrant of (dir.x, dir.y), each
 // pre-ordered (near, far) for rays of that quadrant; a ray reads the copy of
-// its quadrant, so the box test pairs only the z planes by min/max (16 fewer
-// VALU ops per node).  Slab distances are monotone in the plane coordinate
+// its quadrant (and, MRT_ZSEL, its z rows in ray order by a row offset), so
+// the box test pairs no planes by min/max (24 fewer VALU ops per node).
+// Slab distances are monotone in the plane coordinate
 // for a fixed direction (in both builds), so the quadrant's near plane is
 // exactly the min of the pair and results are bit-identical.  (Eight octant
 // copies measured -7.5 % on C2: the larger LDS image cost a resident block.)
