@@ -46,6 +46,7 @@
 #include <fstream>
 #include <sstream>
 #include <atomic>
+#include <mutex>
 
 namespace {
 
@@ -122,6 +123,11 @@ struct Scene {
   std::vector<LightTriangle> lightTriangles;   // includes the sentinel
   uint32_t lightTrianglesCount = 0;
   std::string error;
+  // Triangle planes (v0, e1 = v1 - v0, e2 = v2 - v0) in SoA form for the
+  // packet brute force of large scenes (built on first use; see
+  // intersect_packet).  The same float values tri_hit derives per test.
+  mutable std::once_flag soa_once;
+  mutable std::vector<float> soa;   // [9][T]
 };
 
 struct MtlColor { float r = 0, g = 0, b = 0; bool set = false; };
@@ -354,6 +360,87 @@ static Intersection intersect_one(const Scene& sc, const float* o3, float tmin, 
   }
   if (found) { r.distance = bt; r.triangleIndex = bk; r.coordinates[0] = bu; r.coordinates[1] = bv; }
   return r;
+}
+
+// The same brute force for a packet of rays over a large scene: triangles in
+// blocks of kPacketBlock (SoA planes, resident in L2) with every ray of the
+// packet tested against a block before the next block streams in.  Each test
+// is tri_hit's arithmetic in a branch-free (vectorisable) form, and triangles
+// are visited in increasing index order per ray with the strict `t < best`
+// rule, so the result is exactly intersect_one's (ties -> lowest index).
+constexpr size_t kPacketBlock = 2048;
+
+static void build_soa(const Scene& sc) {
+  const size_t T = sc.references.size();
+  sc.soa.assign(9 * T, 0.0f);
+  for (size_t k = 0; k < T; ++k) {
+    const uint32_t* tri = sc.references[k].tri;
+    const F3 v0 = f3(sc.vertices[tri[0]].v), v1 = f3(sc.vertices[tri[1]].v), v2 = f3(sc.vertices[tri[2]].v);
+    const F3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+    const float c[9] = {v0.x, v0.y, v0.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z};
+    for (int j = 0; j < 9; ++j) sc.soa[(size_t)j * T + k] = c[j];
+  }
+}
+
+// hit flags and distances of one ray against triangles [b, e) (branch free)
+__attribute__((target_clones("avx512f", "avx2", "default")))
+static uint32_t block_tests(const float* __restrict__ soa, size_t T, size_t b, size_t e, F3 o, F3 d, float tmin,
+                        float tmax, float* __restrict__ t_out, uint8_t* __restrict__ hit_out) {
+  const float* __restrict__ v0x = soa + b; const float* __restrict__ v0y = soa + T + b;
+  const float* __restrict__ v0z = soa + 2 * T + b; const float* __restrict__ e1x = soa + 3 * T + b;
+  const float* __restrict__ e1y = soa + 4 * T + b; const float* __restrict__ e1z = soa + 5 * T + b;
+  const float* __restrict__ e2x = soa + 6 * T + b; const float* __restrict__ e2y = soa + 7 * T + b;
+  const float* __restrict__ e2z = soa + 8 * T + b;
+  const size_t n = e - b;
+  uint32_t hits = 0;
+  for (size_t k = 0; k < n; ++k) {
+    // p = cross(d, e2); det = dot(e1, p)
+    const float px = d.y * e2z[k] - d.z * e2y[k], py = d.z * e2x[k] - d.x * e2z[k], pz = d.x * e2y[k] - d.y * e2x[k];
+    const float det = (e1x[k] * px + e1y[k] * py) + e1z[k] * pz;
+    const float inv = 1.0f / det;
+    const float sx = o.x - v0x[k], sy = o.y - v0y[k], sz = o.z - v0z[k];
+    const float b1 = ((sx * px + sy * py) + sz * pz) * inv;
+    // q = cross(s, e1)
+    const float qx = sy * e1z[k] - sz * e1y[k], qy = sz * e1x[k] - sx * e1z[k], qz = sx * e1y[k] - sy * e1x[k];
+    const float b2 = ((d.x * qx + d.y * qy) + d.z * qz) * inv;
+    const float tt = ((e2x[k] * qx + e2y[k] * qy) + e2z[k] * qz) * inv;
+    const bool hit = (det != 0.0f) & (b1 >= 0.0f) & (b1 <= 1.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f) &
+                     (tt >= tmin) & (tt <= tmax);
+    t_out[k] = tt;
+    hit_out[k] = hit;
+    hits += hit;
+  }
+  return hits;
+}
+
+static void intersect_packet(const Scene& sc, const float* const* o3, const float* tmin, const float* const* d3,
+                             const float* tmax, size_t n, Intersection* out) {
+  std::call_once(sc.soa_once, build_soa, std::cref(sc));
+  const size_t T = sc.references.size();
+  std::vector<uint8_t> found(n, 0);
+  std::vector<float> bt(n, 0.0f);
+  std::vector<uint32_t> bk(n, 0);
+  float t_blk[kPacketBlock];
+  uint8_t hit_blk[kPacketBlock];
+  for (size_t b = 0; b < T; b += kPacketBlock) {
+    const size_t e = std::min(T, b + kPacketBlock);
+    for (size_t r = 0; r < n; ++r) {
+      if (tmax[r] < 0.0f) continue;
+      if (!block_tests(sc.soa.data(), T, b, e, f3(o3[r]), f3(d3[r]), tmin[r], tmax[r], t_blk, hit_blk)) continue;
+      for (size_t k = 0; k < e - b; ++k)
+        if (hit_blk[k] && (!found[r] || t_blk[k] < bt[r])) { found[r] = 1; bt[r] = t_blk[k]; bk[r] = (uint32_t)(b + k); }
+    }
+  }
+  for (size_t r = 0; r < n; ++r) {
+    if (!found[r]) { out[r] = Intersection{-1.0f, 0xFFFFFFFFu, {0.0f, 0.0f}}; continue; }
+    // (u, v) of the winning triangle: tri_hit's own expressions
+    const uint32_t* tri = sc.references[bk[r]].tri;
+    float t, u, v;
+    const bool ok = tri_hit(f3(o3[r]), f3(d3[r]), f3(sc.vertices[tri[0]].v), f3(sc.vertices[tri[1]].v),
+                            f3(sc.vertices[tri[2]].v), tmin[r], tmax[r], t, u, v);
+    (void)ok;
+    out[r] = Intersection{bt[r], bk[r], {u, v}};
+  }
 }
 
 // ============================================================================
@@ -621,6 +708,11 @@ extern "C" {
 
 struct orc_scene { Scene s; };
 
+// Scenes with at least this many triangles are rendered by orc_render in row
+// packets (intersect_packet); tests lower it to check both forms agree.
+static size_t g_packet_threshold = 4096;
+void orc_set_packet_threshold(uint64_t triangles) { g_packet_threshold = (size_t)triangles; }
+
 int orc_scene_load(const char* obj_path, const char* mtl_override, orc_scene** out) {
   auto* sc = new orc_scene();
   if (!load_scene(obj_path, mtl_override, sc->s)) {
@@ -694,6 +786,19 @@ void orc_raygen(uint32_t W, uint32_t H, const float* noise, void* rays) {
 void orc_intersect(const orc_scene* sc, const void* rays, uint32_t stride, uint32_t count, void* isect_out) {
   const uint8_t* p = (const uint8_t*)rays;
   Intersection* out = (Intersection*)isect_out;
+  if (sc->s.references.size() >= g_packet_threshold) {   // large scene: packets of 256 rays
+    std::vector<const float*> op(256), dp(256);
+    std::vector<float> tmn(256), tmx(256);
+    for (uint32_t i0 = 0; i0 < count; i0 += 256) {
+      const uint32_t n = std::min<uint32_t>(256, count - i0);
+      for (uint32_t j = 0; j < n; ++j) {
+        const float* f = (const float*)(p + (size_t)(i0 + j) * stride);
+        op[j] = f; tmn[j] = f[3]; dp[j] = f + 4; tmx[j] = f[7];
+      }
+      intersect_packet(sc->s, op.data(), tmn.data(), dp.data(), tmx.data(), n, out + i0);
+    }
+    return;
+  }
   for (uint32_t i = 0; i < count; ++i) {
     const float* f = (const float*)(p + (size_t)i * stride);
     out[i] = intersect_one(sc->s, f, f[3], f + 4, f[7]);
@@ -734,6 +839,7 @@ int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLeng
                uint32_t frame_begin, uint32_t frame_end, uint32_t threads, const uint8_t* pixel_mask,
                float* image_rgba, uint64_t* active_out) {
   if (W < 2 || H < 2 || maxPathLength == 0) return -1;
+  const bool use_packets = sc->s.references.size() >= g_packet_threshold;
   NoiseCache nc{seed, {}};
   std::atomic<uint64_t> active{0};
   if (threads == 0) threads = 1;
@@ -742,7 +848,46 @@ int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLeng
     std::vector<const float*> iterNoise(maxPathLength);
     for (uint32_t i = 0; i < maxPathLength; ++i) iterNoise[i] = nc.get(noise_frame_for(f, i));
     std::atomic<uint32_t> next_row{0};
+    // large scenes: each row is one packet through the stages (the per-pixel
+    // operations and their order are the same; only pixels interleave)
+    auto work_packets = [&]() {
+      uint64_t local = 0;
+      std::vector<Ray> rays;
+      std::vector<LightSamplingRay> srays;
+      std::vector<uint32_t> xs;
+      std::vector<Intersection> is;
+      std::vector<const float*> op, dp;
+      std::vector<float> tmn, tmx;
+      auto trace = [&](bool shadow) {
+        const size_t n = xs.size();
+        for (size_t j = 0; j < n; ++j) {
+          if (shadow) { op[j] = srays[j].origin; dp[j] = srays[j].direction; tmn[j] = srays[j].minDistance; tmx[j] = srays[j].maxDistance; }
+          else { op[j] = rays[j].origin; dp[j] = rays[j].direction; tmn[j] = rays[j].minDistance; tmx[j] = rays[j].maxDistance; }
+        }
+        intersect_packet(sc->s, op.data(), tmn.data(), dp.data(), tmx.data(), n, is.data());
+      };
+      for (uint32_t y = next_row++; y < H; y = next_row++) {
+        xs.clear();
+        for (uint32_t x = 0; x < W; ++x)
+          if (!pixel_mask || pixel_mask[(size_t)y * W + x]) xs.push_back(x);
+        const size_t n = xs.size();
+        if (!n) continue;
+        rays.assign(n, Ray{}); srays.assign(n, LightSamplingRay{}); is.resize(n);
+        op.resize(n); dp.resize(n); tmn.resize(n); tmx.resize(n);
+        for (size_t j = 0; j < n; ++j) rayGenerator(rays[j], xs[j], y, W, H, raygenNoise);
+        for (uint32_t i = 0; i < maxPathLength; ++i) {
+          for (size_t j = 0; j < n; ++j) local += rays[j].maxDistance >= 0.0f;
+          trace(false);
+          for (size_t j = 0; j < n; ++j) intersectionHandler(sc->s, is[j], rays[j], srays[j], xs[j], y, f, maxPathLength, iterNoise[i]);
+          trace(true);
+          for (size_t j = 0; j < n; ++j) lightSamplingHandler(is[j], rays[j], srays[j]);
+        }
+        for (size_t j = 0; j < n; ++j) accumulateImage(rays[j], image_rgba + 4 * ((size_t)y * W + xs[j]), f);
+      }
+      active += local;
+    };
     auto work = [&]() {
+      if (use_packets) { work_packets(); return; }
       uint64_t local = 0;
       for (uint32_t y = next_row++; y < H; y = next_row++)
         for (uint32_t x = 0; x < W; ++x) {

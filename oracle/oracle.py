@@ -83,6 +83,7 @@ def lib() -> ctypes.CDLL:
         L.orc_resolve.argtypes = [u32, vp, vp, vp]
         L.orc_accumulate.argtypes = [u32, u32, vp, vp]
         L.orc_render.argtypes = [vp, u32, u32, u32, u64, u32, u32, u32, vp, vp, vp]
+        L.orc_set_packet_threshold.argtypes = [u64]
         _lib = L
     return _lib
 
@@ -158,6 +159,16 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError("orc_render failed")
         return image, int(active[0])
+
+
+PACKET_THRESHOLD = 4096   # orc_render / orc_intersect default (triangles)
+
+
+def set_packet_threshold(triangles: int) -> None:
+    """Scenes with at least this many triangles are brute-forced in ray
+    packets over SoA triangle blocks (same answers, far faster on 1M
+    triangles); tests move it to check both forms agree."""
+    lib().orc_set_packet_threshold(triangles)
 
 
 def noise_table(seed: int, frame: int) -> np.ndarray:

@@ -141,3 +141,32 @@ def test_active_rays_bounded(cornell):
     for L in (1, 2, 4):
         _, A = cornell.render(W, H, L, SEED, 1)
         assert W * H <= A <= W * H * L
+
+
+def test_packet_bruteforce_equals_per_ray(oracle_mod, mrt_mod):
+    """The packet form of the brute-force nearest hit (SoA triangle blocks,
+    branch-free tests, used for the 1M-triangle scenes) answers bit for bit
+    like the per-ray form, for intersections and whole renders."""
+    s = mrt_mod.Scene("cornellbox", procedural_triangles=8192, procedural_seed=11, device=-1)
+    e = s.export()
+    osc = oracle_mod.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
+    rng = np.random.default_rng(1)
+    n = 3000
+    rays = np.zeros(n, oracle_mod.RAY_DTYPE)
+    rays["origin"] = rng.uniform([-0.95, 0.05, -0.95], [0.95, 1.95, 2.3], size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    rays["direction"] = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    rays["maxDistance"] = np.float32(np.inf)
+    rays["maxDistance"][::7] = -1.0
+    rays["maxDistance"][3::11] = 0.3
+    rays["direction"][1::29] = np.float32([0.0, 1.0, 0.0])
+    out = {}
+    try:
+        for thr in (1 << 40, 0):
+            oracle_mod.set_packet_threshold(thr)
+            out[thr] = (osc.intersect(rays), osc.render(40, 30, 8, SEED, 2, threads=4))
+    finally:
+        oracle_mod.set_packet_threshold(oracle_mod.PACKET_THRESHOLD)
+    (i1, (img1, a1)), (i2, (img2, a2)) = out[1 << 40], out[0]
+    assert i1.tobytes() == i2.tobytes() and (i1["distance"] > 0).mean() > 0.3
+    assert img1.tobytes() == img2.tobytes() and a1 == a2
