@@ -31,7 +31,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRT_LIB") or os.path.join(HERE, "lib", "libmrt.so")   # MRT_LIB: diagnostic builds
 INCLUDE_H = os.path.join(os.path.dirname(HERE), "include", "mrt.h")
-SCENES_DIR = os.path.join(os.path.dirname(HERE), "tests", "golden", "scenes")
+SCENES_DIR = os.path.join(HERE, "scenes")   # renderer/Media scene data, rendered unchanged
 
 FLAG_PRECISE = 1
 FLAG_PROFILE = 2
@@ -203,7 +203,8 @@ def _check(rc: int, what: str) -> None:
 
 
 def scene_path(name: str) -> str:
-    """Path of a scene shipped under tests/golden/scenes (renderer/Media data)."""
+    """Path of a scene shipped with the package (metal-renderer_amd/scenes: the
+    reference's renderer/Media OBJ/MTL data files, unchanged)."""
     return name if os.path.sep in name else os.path.join(SCENES_DIR, name if name.endswith(".obj") else name + ".obj")
 
 

@@ -7,9 +7,10 @@ Fixture contents (data only: inputs/expected outputs):
   * per golden: banner-masked mean linear RGB, peak, and a 40x30 block-mean
     image (20x20-pixel blocks of the 800x600 image, row 0 = TOP, banner
     masked to 0 — the same mask is applied to our renders before comparing).
-  * the scene OBJ/MTL files are NOT copied; tests that need a scene use
-    tests/golden/scenes/ (small copies of renderer/Media data files:
-    cornellbox.obj/.mtl, white-box.obj — data fixtures the reference holds).
+  * the scene OBJ/MTL data files the reference ships (renderer/Media/*.obj,
+    *.mtl) are copied unchanged into metal-renderer_amd/scenes/: they are the
+    product's input data ("scenes in renderer/Media render unchanged"), not
+    source code.
 """
 from __future__ import annotations
 
@@ -56,7 +57,7 @@ def main():
     with open(os.path.join(HERE, "golden_stats.json"), "w") as f:
         json.dump(stats, f, indent=1, sort_keys=True)
     # scene data files the reference ships (inputs, not source code)
-    sdir = os.path.join(HERE, "scenes")
+    sdir = os.path.join(os.path.dirname(os.path.dirname(HERE)), "metal-renderer_amd", "scenes")
     os.makedirs(sdir, exist_ok=True)
     for fn in ("cornellbox.obj", "cornellbox.mtl", "white-box.obj", "CornellBox-Water-plastic.obj",
                "CornellBox-Water-plastic.mtl", "CornellBox-Water-mirror.obj", "CornellBox-Water-mirror.mtl",

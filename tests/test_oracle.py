@@ -13,9 +13,6 @@ import pytest
 
 from helpers import SEED, compare_to_golden
 
-SCENES = "tests/golden/scenes"
-
-
 @pytest.fixture(scope="module")
 def cornell(oracle_mod, mrt_mod):
     return oracle_mod.OracleScene(mrt_mod.scene_path("cornellbox"))

@@ -118,7 +118,7 @@ static Counts trace(const BvhResult& b, V o, V d) {
 }
 
 int main(int argc, char** argv) {
-  const std::string obj = argc > 1 ? argv[1] : "../tests/golden/scenes/cornellbox.obj";
+  const std::string obj = argc > 1 ? argv[1] : "../metal-renderer_amd/scenes/cornellbox.obj";
   const uint32_t proc = argc > 2 ? (uint32_t)atoi(argv[2]) : 0;
   const uint32_t leaf = argc > 3 ? (uint32_t)atoi(argv[3]) : 4;
   const uint32_t width = argc > 4 ? (uint32_t)atoi(argv[4]) : 2;
