@@ -108,23 +108,41 @@ def _cpu_model():
     return "unknown"
 
 
+def host_threads():
+    """The CPUs this process may run on: the affinity mask, capped by the
+    worker-pool size the GPU box sets for one GPU's share (OMP_NUM_THREADS=16
+    there; os.cpu_count() reports the whole 256-CPU machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
 def cpu_baseline(cfg, frames):
     """The CPU oracle (scalar C++ restatement of the path, oracle/; brute-force
     nearest hit in place of MPS) timed on this host on a bounded sample of the
     same workload: C2 runs in full (all `frames` = spp frames
-    of the whole image) on `threads` std::threads over rows, and 2 frames on
+    of the whole image) on every CPU of the process's share, and 2 frames on
     one thread give the scalar rate.  Scenes with more triangles run one frame
-    of a row band sized to ~10 s on all threads and ~10 s on one."""
+    of a row band sized to ~10 s on all threads and ~10 s on one.
+    Returns (baseline dict, oracle image, pixel mask, frames) — the image is
+    kept for the parity check of the GPU render (main)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle  # test/baseline infrastructure only (see oracle/mrt_oracle.cpp header)
     import mrt
     if not os.path.exists(oracle.LIB_PATH):
         oracle.build()
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+    threads = host_threads()
     if cfg["procedural"]:
-        return None   # brute force over 1M triangles is not a bounded sample
-    sc = oracle.OracleScene(mrt.scene_path(cfg["scene"]), resolve_mtl(cfg))
+        # the product's flattened scene (the seeded procedural mesh is built by
+        # libmrt's scene import; the oracle brute-forces the same buffers)
+        e = mrt.Scene(cfg["scene"], resolve_mtl(cfg), procedural_triangles=cfg["procedural"], device=-1).export()
+        sc = oracle.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
+    else:
+        sc = oracle.OracleScene(mrt.scene_path(cfg["scene"]), resolve_mtl(cfg))
     W, H = cfg["width"], cfg["height"]
     if sc.n_triangles <= 64:
         rows = H                      # C2: the whole workload (all spp frames)
@@ -132,18 +150,20 @@ def cpu_baseline(cfg, frames):
         f1 = min(2, frames)
     else:
         # brute force costs ~ (bounces x 2 traversals x triangles) tests per
-        # path at ~1.6e8 tests/s per thread: size the sample to ~10 s on all
-        # threads (one frame of a row band) and ~10 s on one thread
+        # path at ~1.6e8 tests/s per thread (per-ray form) or ~5e8 (packet
+        # form, scenes >= oracle.PACKET_THRESHOLD triangles): size the sample
+        # to ~10 s on all threads (one frame of a row band) and ~10 s on one
         frames = 1
+        rate = 5e8 if sc.n_triangles >= oracle.PACKET_THRESHOLD else 1.6e8
         per_path = min(cfg["L"], 5) * 2 * sc.n_triangles
-        rows = max(1, min(H, int(10.0 * 1.6e8 * threads / (per_path * W))))
+        rows = max(1, min(H, int(10.0 * rate * threads / (per_path * W))))
         rows1 = max(1, rows // threads)
         f1 = 1
     mask = np.zeros((H, W), np.uint8)
     y0 = (H - rows) // 2
     mask[y0:y0 + rows] = 1
     t0 = time.perf_counter()
-    sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads, pixel_mask=mask)
+    img, _ = sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads, pixel_mask=mask)
     dt = time.perf_counter() - t0
     paths = W * rows * frames
     mask1 = np.zeros((H, W), np.uint8)
@@ -151,13 +171,37 @@ def cpu_baseline(cfg, frames):
     t1 = time.perf_counter()
     sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, f1, threads=1, pixel_mask=mask1)
     dt1 = time.perf_counter() - t1
-    return {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+    base = {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
             "single_thread_value": round(W * rows1 * f1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
             "cpu_model": _cpu_model(),
             "sample": f"frames 0-{frames - 1}, rows {y0}-{y0 + rows - 1} of the workload ({W}x{rows} of {W}x{H}, "
                       f"L={cfg['L']}, {paths} paths), brute-force nearest hit over {sc.n_triangles} triangles, "
-                      f"{threads} std::threads over rows, {dt:.2f} s wall; single thread: frames 0-{f1 - 1} "
-                      f"of rows {y0}-{y0 + rows1 - 1}, {dt1:.2f} s"}
+                      f"{threads} std::threads over rows (the process's CPU share: affinity "
+                      f"{len(os.sched_getaffinity(0))}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS', '-')}), "
+                      f"{dt:.2f} s wall; single thread: frames 0-{f1 - 1} of rows {y0}-{y0 + rows1 - 1}, {dt1:.2f} s"}
+    return base, img, mask, frames
+
+
+def image_parity(gpu_img, ref_img, mask, build, frames, note):
+    """Per-pixel relative L2 ||g - c|| / (||c|| + 1e-3) over RGB on the oracle's
+    pixels (BASELINE.md image-match criterion), NaN-aware."""
+    import numpy as np
+    m = mask.astype(bool)
+    g = gpu_img[m][:, :3].astype(np.float64)
+    c = ref_img[m][:, :3].astype(np.float64)
+    both_nan = np.isnan(g).any(-1) & np.isnan(c).any(-1)
+    g, c = np.nan_to_num(g), np.nan_to_num(c)
+    rel = np.where(both_nan, 0.0, np.sqrt(((g - c) ** 2).sum(-1)) / (np.sqrt((c ** 2).sum(-1)) + 1e-3))
+    rmse = float(np.sqrt(((g - c) ** 2).mean()) / (np.sqrt((c ** 2).mean()) + 1e-12))
+    same = float(((gpu_img[m][:, :3].view(np.uint32) == ref_img[m][:, :3].view(np.uint32)).all(-1) | both_nan).mean())
+    return {"build": build, "vs": "CPU oracle (cpu_baseline leg's image)", "frames": frames, "pixels": int(m.sum()),
+            "frac_rel_l2_le_1e-2": round(float((rel <= 1e-2).mean()), 6),
+            "frac_rel_l2_le_1e-4": round(float((rel <= 1e-4).mean()), 6), "rel_rmse": float(f"{rmse:.3e}"),
+            "bit_identical": round(same, 6), "max_rel_l2": float(f"{float(rel.max()):.3e}"),
+            "gate": "fast: >= 0.99 of pixels within rel-L2 1e-2; precise: >= 0.999 within 1e-4 and rel-RMSE <= 1e-3",
+            "pass": bool((rel <= 1e-2).mean() >= 0.99) if build == "fast" else
+                    bool((rel <= 1e-4).mean() >= 0.999 and rmse <= 1e-3),
+            "note": note}
 
 
 def main():
@@ -327,11 +371,25 @@ def main():
     avg_launch_ms = kms / max(1, timed)
     achieved = (bytes_alg / max(1, launches)) / (avg_launch_ms * 1e-3) / 1e9 if timed else 0.0
     achieved_job = bytes_alg / elapsed / 1e9
-    traffic = None
+    # PMC-measured figures of the same command (tools/profile.sh ->
+    # tools/prof_summary.py -> profiles/pmc_<config>.json, which records the
+    # commit it was taken at): HBM (fabric) bytes per launch and the VALU
+    # issue share.  rocprofv3 --pmc has to wrap the process, so they cannot
+    # come from this run; "source" says where they did come from.
+    traffic, counter = None, None
     pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and not args.precise:
         with open(pmc_path) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_launch")
+        if traffic and timed:
+            gbs = traffic / (avg_launch_ms * 1e-3) / 1e9
+            counter = {"hbm_bytes_per_launch": traffic, "hbm_gbs": round(gbs, 1),
+                       "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                       "traffic_over_alg_bytes": round(traffic / max(1, bytes_alg / max(1, launches)), 3),
+                       "valu_issue_frac": pmc.get("valu_issue_frac"), "wait_frac": pmc.get("wait_any_frac"),
+                       "source": f"profiles/{os.path.basename(pmc_path)} (tag {pmc.get('tag')}, "
+                                 f"commit {pmc.get('commit', 'unrecorded')})"}
 
     result = {
         "metric": METRIC,
@@ -355,8 +413,17 @@ def main():
                    "bvh": {"builder": {"sah": "host-sah", "lbvh": "device-lbvh", "ploc": "device-ploc"}[args.bvh],
                            "build_ms": round(scene.info["build_ms"], 2), "nodes": scene.info["bvh_nodes"],
                            "max_stack": scene.info["bvh_max_stack"]}},
+        # achieved / frac: ALGORITHMIC bytes (112 B per path + 312 B
+        # per active ray-bounce, the reference's wavefront data contract) per
+        # launch / HIP-event launch time — an equivalent bandwidth, not the
+        # bytes the fused kernel moves; "counter" holds the PMC-measured HBM
+        # rate (far lower: hits and shadow rays stay in registers) and the VALU
+        # issue share, which is what actually bounds the kernel
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "achieved_is": "algorithmic bytes per launch / launch time (equivalent bandwidth)",
+                     "counter": counter,
+                     "limiter": "VALU issue + memory latency of BVH traversal (not HBM bandwidth)",
                      "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),
                      "kernel": "bounce_kernel", "launches": launches, "timed_launches": timed,
                      "avg_launch_ms": round(avg_launch_ms, 4),
@@ -365,7 +432,27 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_frames or (spp if args.config in ("c1", "c2") else 8))
+        base_cpu, ref_img, mask, frames = cpu_baseline(cfg, args.cpu_frames or spp)
+        result["cpu_baseline"] = base_cpu
+        # image match vs the reference restatement (north_star): the timed
+        # render itself when the oracle ran the whole workload (C2: all spp
+        # frames, every pixel), else a render of the sampled frames; and the
+        # same frames through the parity (precise) build
+        par = []
+        for precise in (args.precise, True) if not args.precise else (True,):
+            if not precise and frames == spp:
+                gimg = r.read_image()
+                note = "the timed steps' image (last step: reset + all spp frames)"
+            else:
+                r1 = mrt.Renderer(scene, W, H, L, precise=precise)
+                r1.draw(frames)
+                gimg = r1.read_image()
+                r1.close()
+                note = f"a separate render of frames 0-{frames - 1}"
+            par.append(image_parity(gimg, ref_img, mask, "precise" if precise else "fast", frames, note))
+        result["parity"] = par[0]
+        if len(par) > 1:
+            result["parity_precise"] = par[1]
     if world > 1 and args.check_image:
         if rank == 0:   # the exchanged image == one device rendering the whole frame, bitwise
             ref = torch.zeros_like(image)

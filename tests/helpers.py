@@ -74,3 +74,14 @@ def compare_to_golden(img_bottom_up: np.ndarray, name: str):
     gold = golden_blocks(name).astype(np.float64)
     block_rel_mae = np.abs(blocks - gold).mean() / gold.mean()
     return mean_ours / mean_gold, block_rel_mae
+
+
+def host_threads(cap: int = 16) -> int:
+    """Oracle threads: the CPUs this process may run on, at most `cap` (the
+    GPU box's CPU share for one GPU is 16; os.cpu_count() there reports the
+    whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(cap, n))

@@ -1,0 +1,145 @@
+"""GPU: the BASELINE.json configurations at their own scale against the oracle.
+
+* C2 (the headline: cornellbox 1920x1080, L = 4) rendered at FULL size,
+  8 frames, precise build vs the CPU oracle (BASELINE.md parity gate:
+  per-pixel relative L2 <= 1e-4 on >= 99.9 % of pixels, whole-image relative
+  RMSE <= 1e-3, identical active ray-bounce count A) and fast build vs the
+  same oracle image (relative L2 <= 1e-2 on >= 99 % of pixels);
+* C4/C5's 1M-triangle procedural scene (deep BVH, top nodes in LDS, the rest
+  from global memory, traversal stack spilling to global memory) against the
+  oracle's brute force over all 1,048,612 triangles, L = 4 (C4) and L = 8
+  (C5), precise build;
+* C5's tile sharding: 8 shards of the 4K frame at L = 8 sum bitwise to the
+  1-GPU image;
+* C4 at full size is deterministic and finite;
+* frames in flight (MRT_INFLIGHT = 2, 3: frame batches on separate streams,
+  accumulation chained by events, renderer/Renderer.mm:16,593-600) render
+  bitwise like one stream.
+The oracle runs on the host's CPU share (helpers.host_threads)."""
+import numpy as np
+import pytest
+
+from helpers import SEED, host_threads, pixel_metrics
+
+pytestmark = pytest.mark.gpu
+
+C2 = dict(W=1920, H=1080, L=4, frames=8)
+PROC = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def c2_oracle(oracle_mod, mrt_mod):
+    osc = oracle_mod.OracleScene(mrt_mod.scene_path("cornellbox"))
+    return osc.render(C2["W"], C2["H"], C2["L"], SEED, C2["frames"], threads=host_threads())
+
+
+@pytest.mark.parametrize("build", ["precise", "fast"])
+def test_c2_full_size_matches_oracle(gpu, mrt_mod, c2_oracle, build):
+    ref, A = c2_oracle
+    sc = mrt_mod.Scene("cornellbox")
+    r = mrt_mod.Renderer(sc, C2["W"], C2["H"], C2["L"], precise=(build == "precise"))
+    r.draw(C2["frames"])
+    img, st = r.read_image(), r.stats()
+    r.close()
+    rel, rmse, same = pixel_metrics(img, ref)
+    print(f"C2 full size {build}: bit-identical {same:.6f}, rel<=1e-4 {np.mean(rel <= 1e-4):.6f}, "
+          f"rel<=1e-2 {np.mean(rel <= 1e-2):.6f}, rmse {rmse:.2e}, A {st['active_ray_bounces']} vs {A}")
+    assert np.isfinite(img).all()
+    if build == "precise":
+        assert np.mean(rel <= 1e-4) >= 0.999 and rmse <= 1e-3
+        assert st["active_ray_bounces"] == A
+    else:
+        assert np.mean(rel <= 1e-2) >= 0.99
+        assert abs(st["active_ray_bounces"] - A) <= A // 1000
+
+
+@pytest.fixture(scope="module")
+def big_scene(gpu, mrt_mod, oracle_mod):
+    """C4/C5's scene: cornellbox + the seeded 1M-triangle displaced sphere
+    (host SAH BVH4), and the oracle over the same flattened buffers."""
+    sc = mrt_mod.Scene("cornellbox", procedural_triangles=PROC)
+    e = sc.export()
+    osc = oracle_mod.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
+    assert sc.info["triangles"] == PROC + 36
+    assert sc.info["bvh_nodes"] > sc.info["bvh_lds_nodes"] > 0
+    return sc, osc
+
+
+@pytest.mark.parametrize("L", [4, 8], ids=["C4-L4", "C5-L8"])
+def test_1m_triangles_match_bruteforce_oracle(big_scene, mrt_mod, L):
+    sc, osc = big_scene
+    W, H, frames = 64, 48, 2
+    ref, A = osc.render(W, H, L, SEED, frames, threads=host_threads())
+    r = mrt_mod.Renderer(sc, W, H, L, precise=True)
+    r.draw(frames)
+    img, st = r.read_image(), r.stats()
+    r.close()
+    rel, rmse, same = pixel_metrics(img, ref)
+    print(f"1M tris L={L}: bit-identical {same:.5f}, rel<=1e-4 {np.mean(rel <= 1e-4):.5f}, rmse {rmse:.2e}, "
+          f"A {st['active_ray_bounces']} vs {A}, max_stack {sc.info['bvh_max_stack']}")
+    assert np.mean(rel <= 1e-4) >= 0.999 and rmse <= 1e-3
+    assert st["active_ray_bounces"] == A
+
+
+def test_c5_shards_sum_to_single_gpu(big_scene, mrt_mod, monkeypatch):
+    """C5: 3840x2160, L = 8, 64x64 tiles over 8 shards; each shard's image
+    holds only its tiles, and the sum is the 1-GPU image bitwise."""
+    sc, _ = big_scene
+    W, H, L, frames, S = 3840, 2160, 8, 2, 8
+    monkeypatch.setenv("MRT_BATCH", str(frames))
+    r = mrt_mod.Renderer(sc, W, H, L)
+    r.draw(frames)
+    full, st_full = r.read_image(), r.stats()
+    r.close()
+    acc = np.zeros_like(full)
+    paths = 0
+    for k in range(S):
+        r = mrt_mod.Renderer(sc, W, H, L, shard_rank=k, shard_count=S)
+        r.draw(frames)
+        part = r.read_image()
+        paths += r.stats()["paths"]
+        r.close()
+        mask, _ = mrt_mod.shard_mask(W, H, k, S)
+        assert not part[mask == 0].any()
+        acc += part
+    assert paths == W * H * frames == st_full["paths"]
+    assert np.isfinite(full).all() and full[..., :3].max() > 0
+    assert np.array_equal(acc[..., :3], full[..., :3]) and np.all(acc[..., 3] == 1.0)
+
+
+def test_c4_full_size_deterministic(big_scene, mrt_mod):
+    sc, _ = big_scene
+    W, H, L, frames = 1920, 1080, 4, 4
+    r = mrt_mod.Renderer(sc, W, H, L)
+    r.draw(frames)
+    a, st = r.read_image(), r.stats()
+    r.reset()
+    r.draw(frames)
+    b, st2 = r.read_image(), r.stats()
+    r.close()
+    assert a.tobytes() == b.tobytes()
+    assert np.isfinite(a).all() and a[..., :3].max() > 0
+    A1 = st["active_ray_bounces"]
+    assert st2["active_ray_bounces"] == 2 * A1 and W * H * frames < A1 < W * H * frames * L
+
+
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_frames_in_flight_bitwise(gpu, mrt_mod, monkeypatch, inflight):
+    """MRT_INFLIGHT = k runs frame batches on k streams; the accumulation is
+    chained in frame order with events, and the next draw's counter resets
+    wait for the joined streams: two consecutive draws of several batches
+    each must equal the single-stream image and counts bitwise."""
+    out = {}
+    for scene, L in (("cornellbox", 4), ("CornellBox-Water-plastic", 8)):
+        sc = mrt_mod.Scene(scene)
+        for k in (1, inflight):
+            monkeypatch.setenv("MRT_INFLIGHT", str(k))
+            monkeypatch.setenv("MRT_BATCH", "2")
+            r = mrt_mod.Renderer(sc, 200, 120, L)
+            r.draw(7)
+            r.draw(5)
+            out[(scene, k)] = (r.read_image(), r.stats()["active_ray_bounces"])
+            r.close()
+        a, b = out[(scene, 1)], out[(scene, inflight)]
+        assert np.isfinite(a[0]).all() and a[0][..., :3].max() > 0
+        assert a[0].tobytes() == b[0].tobytes() and a[1] == b[1], scene
