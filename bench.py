@@ -4,10 +4,13 @@
 Metric (BASELINE.json): Mpaths/s at 1920x1080, 4 bounces (config C2:
 cornellbox, 64 spp, L = 4, diffuse).  One "step" = one complete C2 render:
 reset + 64 frames (1 spp each, L bounce launches per frame) on the tiles this
-rank owns, plus — for N > 1 — the single RCCL reduce of the RGBA32F
-accumulation image to rank 0.  value = paths of all ranks / max-over-ranks
-step time (strong scaling: the frame is split into 64x64 tiles, tile t on
-rank t % N).
+rank owns, plus — for N > 1 — the single RCCL exchange of the accumulation
+image to rank 0, done by libmrt itself (mrt_renderer_exchange: a gather of
+the packed owned tiles, overlapped with the next step's draw; or an in-place
+SUM reduce).  value = paths of all ranks / max-over-ranks step time (strong
+scaling: the frame is split into 64x64 tiles, tile t on rank t % N).
+torch is used only as the CPU control plane for N > 1 (gloo: the RCCL unique
+id broadcast, barriers and the max over ranks); no torch GPU state exists.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c3g|c4|c5]
 For N > 1 launch with torch.distributed.run (one process per GPU).
@@ -78,8 +81,9 @@ def parse():
                    help="N > 1: exchange inside each step instead of overlapping it with the next step's draw")
     p.add_argument("--check-image", action="store_true",
                    help="N>1: rank 0 renders the frame alone afterwards and asserts the exchanged image is bitwise equal")
-    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                   help="gloo = rehearsal of the N>1 path on fewer GPUs (reduce on a host copy)")
+    p.add_argument("--exchange-backend", default="rccl", choices=["rccl", "host"],
+                   help="rccl: libmrt's RCCL collective (one process per GPU); host: packed tiles through host "
+                        "memory and a gloo gather (rehearsal of the N>1 path with several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -217,135 +221,92 @@ def main():
         if world > 1:
             raise SystemExit("--shard-of is a single-process diagnostic")
         shard_count = args.shard_of
-    import torch
-    import torch.distributed as dist
-
-    device = local_rank % max(1, torch.cuda.device_count())   # == local_rank on a full node
-    torch.cuda.set_device(device)
-    torch.cuda.init()           # torch's HIP runtime first, then libmrt's (see mrt.py)
-    import mrt
+    dist = None
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group("gloo")
+        # imported before libmrt is loaded: torch's bundled HIP runtime and
+        # RCCL carry the same sonames as ROCm's, so libmrt binds to the copies
+        # already in the process (one runtime); torch itself never touches the GPU
+        import torch
+        import torch.distributed as dist   # CPU control plane (gloo) only
+    import mrt
+    ndev = mrt.device_count()
+    if ndev == 0:
+        raise SystemExit("no HIP device visible to libmrt")
+    device = local_rank % ndev   # == local_rank on a full node
+    if world > 1:
+        dist.init_process_group("gloo")
     W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
     scene = mrt.Scene(cfg["scene"], resolve_mtl(cfg), procedural_triangles=cfg["procedural"], device=device,
                       bvh_builder={"sah": mrt.BVH_HOST_SAH, "lbvh": mrt.BVH_DEVICE_LBVH,
                                    "ploc": mrt.BVH_DEVICE_PLOC}[args.bvh])
-    # the accumulation image lives in a torch tensor so RCCL can reduce it in
-    # place; libmrt renders into it on its own stream (torch ships its own HIP
-    # runtime copy, so streams are not shared: r.sync() orders the reduce)
-    image = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
-    torch.cuda.synchronize()
     r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True,
-                     shard_rank=(args.shard_rank if args.shard_of else rank), shard_count=shard_count,
-                     image_ptr=image.data_ptr())
+                     shard_rank=(args.shard_rank if args.shard_of else rank), shard_count=shard_count)
     r.prepare(spp)
 
     # multi-GPU exchange: every rank's owned 64x64 tiles go
-    # to rank 0 — by default one RCCL gather of the densely packed tiles
-    # (1/N of the image per rank), or one RCCL SUM reduce of the whole image
-    # (non-owned pixels are 0); both give the 1-GPU image bitwise
-    packed_n = mrt.tiles_packed_floats(W, H, 0, world) if world > 1 else 0   # rank 0 owns the most tiles
-    # --overlap (default for the gather): step k's tiles are packed on the
-    # renderer's stream behind its draw and gathered during step k+1's draw
-    # (double-buffered packed tiles; rank 0 unpacks on the renderer's stream,
-    # non-owned tiles only, so it never touches the pixels being rendered);
-    # the last step's exchange is flushed inside the timed region
-    overlap = world > 1 and args.exchange == "gather" and not args.no_overlap
-    nccl = args.dist_backend == "nccl"
-    rstream = r.stream()
-    if world > 1:
-        tdev = "cuda" if nccl else "cpu"
-        packed = [torch.zeros(packed_n, dtype=torch.float32, device="cuda") for _ in range(2 if overlap else 1)]
-        pack_done = [mrt.Event() for _ in packed]
-        gathered = [torch.zeros(packed_n, dtype=torch.float32, device=tdev) for _ in range(world)] if rank == 0 else None
-        torch.cuda.synchronize()
+    # to rank 0 through libmrt's RCCL communicator (include/mrt.h
+    # mrt_renderer_exchange), enqueued on the renderer's stream behind the
+    # draw.  Default: gather of the densely packed owned tiles (1/N of the
+    # image per rank), MRT_EXCHANGE_OVERLAP — the gather of step k runs on the
+    # communicator's stream while step k+1 renders, and rank 0 unpacks it
+    # (non-owned tiles only) at the next exchange; the packed tiles are
+    # double-buffered and libmrt orders buffer reuse with events.  The last
+    # step's exchange is flushed inside the timed region.
+    comm = None
+    mode = 0
+    if world > 1 and args.exchange_backend == "rccl":
+        uid = [mrt.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = mrt.Comm(uid[0], world, rank, device)
+        mode = (mrt.EXCHANGE_REDUCE if args.exchange == "reduce" else
+                mrt.EXCHANGE_GATHER | (0 if args.no_overlap else mrt.EXCHANGE_OVERLAP))
+    host_slab = mrt.tiles_packed_floats(W, H, 0, world) if world > 1 else 0
 
-    def gather_unpack(i):
-        """The single RCCL gather (xGMI) of buffer i's packed tiles to rank 0,
-        which unpacks them into the image on the renderer's stream."""
-        pack_done[i].synchronize()   # host wait: libmrt's pack of buffer i is complete
-        src = packed[i] if nccl else packed[i].cpu()
-        dist.gather(src, gathered, dst=0)
+    def host_exchange():
+        """Rehearsal transport (ranks may share a GPU): packed tiles to host,
+        one gloo gather to rank 0, which writes them into its image."""
+        mine = r.tiles_read(rank, world)
+        buf = torch.zeros(host_slab, dtype=torch.float32)
+        buf[:mine.size] = torch.from_numpy(mine)
+        lst = [torch.zeros(host_slab, dtype=torch.float32) for _ in range(world)] if rank == 0 else None
+        dist.gather(buf, lst, dst=0)
         if rank == 0:
-            bufs = gathered if nccl else [g.cuda() for g in gathered]
-            torch.cuda.synchronize()   # the gather (and copies) in torch's runtime are complete
             for k in range(1, world):
-                mrt.tiles_unpack(bufs[k].data_ptr(), W, H, k, world, image.data_ptr(), stream=rstream, sync=False)
-            if not nccl:
-                r.sync()   # the temporary device copies are released on return
-
-    def exchange():
-        """One exchange inside the step (--no-overlap, or --exchange reduce)."""
-        torch.cuda.synchronize()   # the previous step's collective has released `packed` / `image`
-        if args.exchange == "reduce":
-            r.sync()
-            if nccl:
-                dist.reduce(image, dst=0)   # the single RCCL reduce of the accumulation image (xGMI)
-            else:
-                host = image.cpu()
-                dist.reduce(host, dst=0)
-                if rank == 0:
-                    image.copy_(host.cuda())
-            torch.cuda.synchronize()
-            return
-        mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed[0].data_ptr(), stream=rstream, sync=False)
-        pack_done[0].record(rstream)
-        gather_unpack(0)
-        r.sync()
-
-    state = {"k": 0, "pending": None}
+                r.tiles_write(k, lst[k].numpy()[:mrt.tiles_packed_floats(W, H, k, world)])
 
     def step():
         r.reset()
         r.draw(spp)
         if world == 1:
             return
-        if not overlap:
-            exchange()
-            return
-        i = state["k"] % 2
-        torch.cuda.synchronize()   # the gather that read packed[i] two steps ago has completed
-        if state["pending"] is not None:
-            gather_unpack(state["pending"])   # the previous step's tiles move while this step renders
-        mrt.tiles_pack(image.data_ptr(), W, H, rank, world, packed[i].data_ptr(), stream=rstream, sync=False)
-        pack_done[i].record(rstream)
-        state["pending"] = i
-        state["k"] += 1
+        if comm is not None:
+            r.exchange(comm, mode)
+        else:
+            host_exchange()
 
-    def flush():
-        if overlap and state["pending"] is not None:
-            torch.cuda.synchronize()
-            gather_unpack(state["pending"])
-            state["pending"] = None
+    def finish():
+        r.exchange_flush()
+        r.sync()
 
     for _ in range(args.warmup):
         step()
-    flush()
-    r.sync()
-    torch.cuda.synchronize()
+    finish()
     base = r.stats()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    flush()
-    r.sync()
-    torch.cuda.synchronize()
+    finish()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = r.stats()
     if world > 1:
-        tdev = "cuda" if args.dist_backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([st["paths"] - base["paths"]], dtype=torch.float64, device=tdev)
+        tot = torch.tensor([st["paths"] - base["paths"]], dtype=torch.float64)
         dist.all_reduce(tot)
         assert int(tot.item()) == W * H * spp * args.steps, "ranks did not cover the frame"
     total_paths = W * H * spp * args.steps
@@ -408,7 +369,8 @@ def main():
                 ", deterministic noise seed",
         "config": {"workload": cfg["workload"], "width": W, "height": H, "spp": spp, "max_path_length": L,
                    "scene": cfg["scene"], "parallelism": (f"tile shard {args.shard_rank} of {shard_count} (one GPU's share)" if args.shard_of else
-                                   f"tiles64x{world}" + (f" + rccl {args.exchange}" if world > 1 else "")),
+                                   f"tiles64x{world}" + ((f" + rccl {args.exchange}" + ("" if args.no_overlap or args.exchange == "reduce" else " (overlapped)")
+                                                          if args.exchange_backend == "rccl" else " + host/gloo gather") if world > 1 else "")),
                    "build": "precise" if args.precise else "fast",
                    "bvh": {"builder": {"sah": "host-sah", "lbvh": "device-lbvh", "ploc": "device-ploc"}[args.bvh],
                            "build_ms": round(scene.info["build_ms"], 2), "nodes": scene.info["bvh_nodes"],
@@ -455,19 +417,20 @@ def main():
             result["parity_precise"] = par[1]
     if world > 1 and args.check_image:
         if rank == 0:   # the exchanged image == one device rendering the whole frame, bitwise
-            ref = torch.zeros_like(image)
-            torch.cuda.synchronize()
-            r1 = mrt.Renderer(scene, W, H, L, precise=args.precise, image_ptr=ref.data_ptr())
+            got = r.read_image()
+            r1 = mrt.Renderer(scene, W, H, L, precise=args.precise)
             r1.draw(spp)
-            r1.sync()
+            ref = r1.read_image()
             r1.close()
-            same = bool(torch.equal(ref.view(-1, 4)[:, :3], image.view(-1, 4)[:, :3]))
+            same = got[..., :3].tobytes() == ref[..., :3].tobytes()
             result["image_check"] = "bitwise equal to the 1-GPU render" if same else "MISMATCH"
             assert same, "exchanged image differs from the single-device render"
         dist.barrier()
     if rank == 0:
         print(json.dumps(result), flush=True)
     r.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

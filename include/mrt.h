@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 3
+#define MRT_ABI_VERSION 4
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -249,6 +249,43 @@ int mrt_tiles_pack(const float* image, uint32_t width, uint32_t height, uint32_t
                    uint32_t shard_count, float* packed, void* stream);
 int mrt_tiles_unpack(const float* packed, uint32_t width, uint32_t height, uint32_t shard_rank,
                      uint32_t shard_count, float* image, void* stream);
+/* ---- multi-GPU exchange through RCCL --------------------
+ * One process per GPU.  Rank 0 makes a unique id, the host distributes its
+ * MRT_COMM_ID_BYTES bytes to every rank (any control channel: MPI, a socket,
+ * torch.distributed gloo), each rank creates its communicator on its device,
+ * and a renderer created with shard_rank = rank, shard_count = nranks
+ * exchanges its accumulation image with one collective, enqueued on the
+ * renderer's stream (no host round trip):
+ *   MRT_EXCHANGE_GATHER — pack the rank's owned 64x64 tiles densely
+ *     (mrt_tiles_pack), one ncclGather of the packed tiles to rank 0
+ *     (1/N of the image per rank; on xGMI rank 0 receives the N-1 slabs
+ *     over N-1 links at once), rank 0 unpacks them into its image;
+ *   MRT_EXCHANGE_REDUCE — one in-place ncclReduce(sum) of the RGBA32F image
+ *     to rank 0 (non-owned pixels are 0, so the sum is the 1-GPU image).
+ * Either way rank 0's image is bitwise the single-device render.
+ * MRT_EXCHANGE_OVERLAP (gather only): the collective runs on the
+ * communicator's own stream after the pack, and rank 0's unpack is deferred
+ * to the next exchange (or mrt_renderer_exchange_flush), so the transfer
+ * overlaps the renderer's next draw; the packed tiles are double-buffered.
+ * The reference has no multi-GPU path (a single Metal device). */
+#define MRT_COMM_ID_BYTES 128
+#define MRT_EXCHANGE_GATHER 1u
+#define MRT_EXCHANGE_REDUCE 2u
+#define MRT_EXCHANGE_OVERLAP 0x100u
+typedef struct mrt_comm mrt_comm;
+int mrt_comm_unique_id(void* id, size_t bytes);   /* ncclGetUniqueId: bytes >= MRT_COMM_ID_BYTES */
+int mrt_comm_create(const void* id, uint32_t nranks, uint32_t rank, int device, mrt_comm** out);
+int mrt_comm_destroy(mrt_comm* comm);
+int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* comm, uint32_t mode);
+/* Complete a deferred (MRT_EXCHANGE_OVERLAP) exchange on the renderer's stream. */
+int mrt_renderer_exchange_flush(mrt_renderer* r);
+/* Host-side exchange for hosts with their own transport (MPI, gloo, ...):
+ * the renderer's owned tiles packed to host memory (mrt_tiles_packed_floats
+ * floats for its shard), and another shard's packed tiles written into the
+ * image.  Both synchronise the renderer. */
+int mrt_renderer_tiles_read(mrt_renderer* r, float* host_packed, size_t floats);
+int mrt_renderer_tiles_write(mrt_renderer* r, uint32_t shard_rank, const float* host_packed, size_t floats);
+
 /* Wait for work queued by libmrt on `stream` (NULL = everything on the device
  * libmrt's runtime has queued). */
 int mrt_synchronize(void* stream);

@@ -11,6 +11,7 @@
 //                        accumulation fused into the bounce where the path
 //                        ends)                                 = L launches
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -66,6 +67,13 @@ hipError_t alloc_isect_spill(DevBuf& b, uint32_t max_stack) {
   return b.alloc((size_t)(max_stack - 32) * mrt::kIntersectSpillGrid * 256 * 4);
 }
 
+#define NCCL_TRY(expr)                                                                            \
+  do {                                                                                            \
+    ncclResult_t e_ = (expr);                                                                     \
+    if (e_ != ncclSuccess)                                                                        \
+      return fail(MRT_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(e_));               \
+  } while (0)
+
 hipError_t upload(DevBuf& b, const void* src, size_t n) {
   hipError_t e = b.alloc(std::max<size_t>(n, 16));
   if (e != hipSuccess) return e;
@@ -120,6 +128,29 @@ struct FrameSlot {
   hipEvent_t acc_done = nullptr;
 };
 
+// RCCL communicator of one rank (one process per GPU) and the stream its
+// overlapped collectives run on
+struct mrt_comm {
+  ncclComm_t comm = nullptr;
+  uint32_t nranks = 0, rank = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+};
+
+// Image exchange state of a renderer (mrt_renderer_exchange): the packed
+// owned tiles, double-buffered so an overlapped gather of step k can still be
+// reading buffer k % 2 while step k + 1 packs into the other, and on rank 0
+// the gathered slabs of every rank.
+struct Exchange {
+  DevBuf packed[2], gathered, staging;
+  hipEvent_t pack_done[2] = {nullptr, nullptr}, gather_done[2] = {nullptr, nullptr};
+  bool gather_recorded[2] = {false, false};
+  uint64_t slab_floats = 0;   // packed floats per rank (rank 0 owns the most tiles)
+  int pending = -1;           // buffer whose gather awaits rank 0's unpack (overlap mode)
+  uint32_t next = 0;
+  const mrt_comm* comm = nullptr;
+};
+
 struct mrt_renderer {
   const mrt_scene* scene = nullptr;
   mrt_renderer_desc desc{};
@@ -150,6 +181,7 @@ struct mrt_renderer {
   mrt_stats stats{};
   uint32_t stack_entries = 32;
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
+  Exchange x;
 };
 
 namespace {
@@ -351,6 +383,50 @@ int write_exr(const char* path, const std::vector<float>& rgba, uint32_t W, uint
   std::fwrite(out.data(), 1, out.size(), f);
   std::fclose(f);
   return MRT_OK;
+}
+
+}  // namespace
+
+namespace {
+
+int exchange_buffers(mrt_renderer* r, const mrt_comm* c) {
+  Exchange& x = r->x;
+  uint64_t floats = 0;
+  if (mrt_tiles_packed_floats(r->desc.width, r->desc.height, 0, c->nranks, &floats)) return MRT_ERR_INVALID;
+  if (x.slab_floats == floats && x.packed[0].p) return MRT_OK;
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  x.slab_floats = floats;
+  for (int i = 0; i < 2; ++i) {
+    HIP_TRY(x.packed[i].alloc(floats * 4));
+    HIP_TRY(hipMemsetAsync(x.packed[i].p, 0, floats * 4, r->stream));   // ranks with fewer tiles send zero padding
+    if (!x.pack_done[i]) HIP_TRY(hipEventCreateWithFlags(&x.pack_done[i], hipEventDisableTiming));
+    if (!x.gather_done[i]) HIP_TRY(hipEventCreateWithFlags(&x.gather_done[i], hipEventDisableTiming));
+    x.gather_recorded[i] = false;
+  }
+  if (c->rank == 0) HIP_TRY(x.gathered.alloc(floats * 4 * c->nranks));
+  return MRT_OK;
+}
+
+// rank 0: unpack every other rank's slab of gather buffer `i` into the image
+// (on the renderer's stream, after the gather); other ranks: order the
+// renderer's stream after the gather so sync/read see it complete
+int exchange_unpack(mrt_renderer* r, int i) {
+  Exchange& x = r->x;
+  const mrt_comm* c = x.comm;
+  HIP_TRY(hipStreamWaitEvent(r->stream, x.gather_done[i], 0));
+  if (c->rank == 0)
+    for (uint32_t k = 1; k < c->nranks; ++k)
+      HIP_TRY(mrt::fast::launch_tiles_move(x.gathered.as<float4>() + (size_t)k * (x.slab_floats / 4),
+                                           reinterpret_cast<float4*>(r->image), r->desc.width, r->desc.height, k,
+                                           c->nranks, false, r->stream));
+  return MRT_OK;
+}
+
+int exchange_flush(mrt_renderer* r) {
+  if (r->x.pending < 0) return MRT_OK;
+  const int i = r->x.pending;
+  r->x.pending = -1;
+  return exchange_unpack(r, i);
 }
 
 }  // namespace
@@ -1115,7 +1191,9 @@ int mrt_renderer_read_image(mrt_renderer* r, float* rgba, size_t count) {
   if (!r || !rgba) return fail(MRT_ERR_INVALID, "null argument");
   const size_t need = (size_t)r->desc.width * r->desc.height * 4;
   if (count < need) return fail(MRT_ERR_INVALID, "output buffer too small");
-  int rc = mrt_renderer_sync(r);
+  int rc = exchange_flush(r);   // a deferred (overlapped) exchange lands first
+  if (rc) return rc;
+  rc = mrt_renderer_sync(r);
   if (rc) return rc;
   HIP_TRY(hipMemcpy(rgba, r->image, need * 4, hipMemcpyDeviceToHost));
   return MRT_OK;
@@ -1146,6 +1224,11 @@ int mrt_renderer_destroy(mrt_renderer* r) {
   if (!r) return MRT_OK;
   (void)finalize_pending(r);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
+  for (int i = 0; i < 2; ++i) {   // an overlapped gather may still read the packed tiles
+    if (r->x.gather_recorded[i]) (void)hipEventSynchronize(r->x.gather_done[i]);
+    if (r->x.pack_done[i]) (void)hipEventDestroy(r->x.pack_done[i]);
+    if (r->x.gather_done[i]) (void)hipEventDestroy(r->x.gather_done[i]);
+  }
   if (r->own_image && r->image) (void)hipFree(r->image);
   for (FrameSlot& fs : r->slots) {
     if (fs.acc_done) (void)hipEventDestroy(fs.acc_done);
@@ -1162,4 +1245,134 @@ int mrt_renderer_destroy(mrt_renderer* r) {
   return MRT_OK;
 }
 
+// ---------------------------------------------------------------------------
+// multi-GPU exchange (RCCL), SURVEY.md §8(e)
+// ---------------------------------------------------------------------------
+int mrt_comm_unique_id(void* id, size_t bytes) {
+  if (!id || bytes < sizeof(ncclUniqueId)) return fail(MRT_ERR_INVALID, "mrt_comm_unique_id: need 128 bytes");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return MRT_OK;
+}
+
+int mrt_comm_create(const void* id, uint32_t nranks, uint32_t rank, int device, mrt_comm** out) {
+  if (!id || !out || nranks == 0 || rank >= nranks || device < 0)
+    return fail(MRT_ERR_INVALID, "mrt_comm_create: bad argument");
+  *out = nullptr;
+  std::unique_ptr<mrt_comm> c(new mrt_comm());
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  const ncclResult_t e = ncclCommInitRank(&c->comm, (int)nranks, u, (int)rank);
+  if (e != ncclSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    return fail(MRT_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(e));
+  }
+  *out = c.release();
+  return MRT_OK;
+}
+
+int mrt_comm_destroy(mrt_comm* c) {
+  if (!c) return MRT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return MRT_OK;
+}
+
+
+int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
+  if (!r || !c) return fail(MRT_ERR_INVALID, "mrt_renderer_exchange: null argument");
+  const uint32_t kind = mode & 0xFFu;
+  const bool overlap = (mode & MRT_EXCHANGE_OVERLAP) != 0;
+  if ((kind != MRT_EXCHANGE_GATHER && kind != MRT_EXCHANGE_REDUCE) || (mode & ~0x1FFu) ||
+      (overlap && kind != MRT_EXCHANGE_GATHER))
+    return fail(MRT_ERR_INVALID, "mrt_renderer_exchange: bad mode");
+  if (c->nranks != r->desc.shard_count || c->rank != r->desc.shard_rank)
+    return fail(MRT_ERR_INVALID, "mrt_renderer_exchange: the renderer's shard (rank, count) must be the comm's");
+  if (c->device != r->scene->device) return fail(MRT_ERR_INVALID, "mrt_renderer_exchange: comm on another device");
+  HIP_TRY(hipSetDevice(c->device));
+  if (r->x.comm && r->x.comm != c) { int rc = exchange_flush(r); if (rc) return rc; }
+  r->x.comm = c;
+  int rc = exchange_flush(r);   // the previous overlapped gather's unpack (rank 0)
+  if (rc) return rc;
+  const uint32_t W = r->desc.width, H = r->desc.height;
+  if (kind == MRT_EXCHANGE_REDUCE) {   // one in-place SUM reduce of the RGBA32F image to rank 0
+    NCCL_TRY(ncclReduce(r->image, r->image, (size_t)W * H * 4, ncclFloat, ncclSum, 0, c->comm, r->stream));
+    return MRT_OK;
+  }
+  rc = exchange_buffers(r, c);
+  if (rc) return rc;
+  Exchange& x = r->x;
+  const int i = overlap ? (int)x.next : 0;
+  x.next ^= 1u;
+  // the gather two exchanges ago may still be reading packed[i]
+  if (x.gather_recorded[i]) HIP_TRY(hipStreamWaitEvent(r->stream, x.gather_done[i], 0));
+  HIP_TRY(mrt::fast::launch_tiles_move(reinterpret_cast<const float4*>(r->image), x.packed[i].as<float4>(), W, H,
+                                       c->rank, c->nranks, true, r->stream));
+  float* recv = c->rank == 0 ? x.gathered.as<float>() : x.packed[i].as<float>();
+  if (overlap) {
+    // the collective waits for the pack (and, on rank 0, for the previous
+    // unpack, which precedes the pack on the renderer's stream) and runs on
+    // the communicator's stream while the renderer's next draw proceeds
+    HIP_TRY(hipEventRecord(x.pack_done[i], r->stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, x.pack_done[i], 0));
+    NCCL_TRY(ncclGather(x.packed[i].p, recv, x.slab_floats, ncclFloat, 0, c->comm, c->stream));
+    HIP_TRY(hipEventRecord(x.gather_done[i], c->stream));
+    x.gather_recorded[i] = true;
+    x.pending = i;
+    return MRT_OK;
+  }
+  NCCL_TRY(ncclGather(x.packed[i].p, recv, x.slab_floats, ncclFloat, 0, c->comm, r->stream));
+  HIP_TRY(hipEventRecord(x.gather_done[i], r->stream));
+  x.gather_recorded[i] = true;
+  return exchange_unpack(r, i);
+}
+
+int mrt_renderer_exchange_flush(mrt_renderer* r) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  return exchange_flush(r);
+}
+
+int mrt_renderer_tiles_read(mrt_renderer* r, float* host, size_t floats) {
+  if (!r || !host) return fail(MRT_ERR_INVALID, "null argument");
+  uint64_t n = 0;
+  int rc = mrt_tiles_packed_floats(r->desc.width, r->desc.height, r->desc.shard_rank, r->desc.shard_count, &n);
+  if (rc) return rc;
+  if (floats < n) return fail(MRT_ERR_INVALID, "mrt_renderer_tiles_read: buffer too small");
+  rc = exchange_flush(r);
+  if (rc) return rc;
+  if (r->x.staging.bytes < n * 4) HIP_TRY(r->x.staging.alloc(n * 4));
+  HIP_TRY(mrt::fast::launch_tiles_move(reinterpret_cast<const float4*>(r->image), r->x.staging.as<float4>(),
+                                       r->desc.width, r->desc.height, r->desc.shard_rank, r->desc.shard_count, true,
+                                       r->stream));
+  HIP_TRY(hipMemcpyAsync(host, r->x.staging.p, n * 4, hipMemcpyDeviceToHost, r->stream));
+  return mrt_renderer_sync(r);
+}
+
+int mrt_renderer_tiles_write(mrt_renderer* r, uint32_t shard_rank, const float* host, size_t floats) {
+  if (!r || !host) return fail(MRT_ERR_INVALID, "null argument");
+  if (shard_rank >= r->desc.shard_count) return fail(MRT_ERR_INVALID, "mrt_renderer_tiles_write: shard_rank >= shard_count");
+  uint64_t n = 0;
+  int rc = mrt_tiles_packed_floats(r->desc.width, r->desc.height, shard_rank, r->desc.shard_count, &n);
+  if (rc) return rc;
+  if (floats < n) return fail(MRT_ERR_INVALID, "mrt_renderer_tiles_write: buffer too small");
+  rc = exchange_flush(r);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(r->stream));   // the staging buffer may still feed a queued copy
+  if (r->x.staging.bytes < n * 4) HIP_TRY(r->x.staging.alloc(n * 4));
+  HIP_TRY(hipMemcpyAsync(r->x.staging.p, host, n * 4, hipMemcpyHostToDevice, r->stream));
+  HIP_TRY(mrt::fast::launch_tiles_move(r->x.staging.as<float4>(), reinterpret_cast<float4*>(r->image), r->desc.width,
+                                       r->desc.height, shard_rank, r->desc.shard_count, false, r->stream));
+  return mrt_renderer_sync(r);
+}
+
 }  // extern "C"
+

@@ -16,11 +16,13 @@ This module only binds the native library: every call runs the HIP kernels in
 libmrt.so.  There is no CPU fallback; if the library is missing the import
 fails loudly.
 
-Interop note: PyTorch-ROCm wheels bundle their own copy of the HIP runtime.
-Both copies share the process's HSA runtime, so device pointers (torch tensors)
-can be handed to libmrt, but (1) torch must initialise its runtime before
-libmrt is first used in a process that uses both, and (2) torch stream handles
-must not be passed to libmrt (synchronise with Renderer.sync() instead).
+Interop note: PyTorch-ROCm wheels bundle their own HIP runtime, HSA runtime
+and RCCL under the same sonames as ROCm's (libamdhip64.so.7, librccl.so.1), so
+a process holds ONE copy of each — whichever was loaded first (checked in
+/proc/self/maps: with torch imported first, libmrt binds to torch/lib's
+copies).  Device pointers (torch tensors) can therefore be handed to libmrt;
+the tests import torch first (the order that is exercised), and synchronise
+libmrt's work with Renderer.sync() / synchronize() rather than torch streams.
 """
 from __future__ import annotations
 
@@ -35,6 +37,8 @@ SCENES_DIR = os.path.join(HERE, "scenes")   # renderer/Media scene data, rendere
 
 FLAG_PRECISE = 1
 FLAG_PROFILE = 2
+COMM_ID_BYTES = 128
+EXCHANGE_GATHER, EXCHANGE_REDUCE, EXCHANGE_OVERLAP = 1, 2, 0x100
 DEFAULT_SEED = 0x6D6574616C2D7274  # "metal-rt"
 
 RAY_BYTES, SHADOW_RAY_BYTES, ISECT_BYTES = 80, 48, 16
@@ -124,6 +128,8 @@ EXPORTED = [
     "mrt_debug_stamps", "mrt_debug_wave_times", "mrt_shard_mask",
     "mrt_tiles_packed_floats", "mrt_tiles_pack", "mrt_tiles_unpack", "mrt_display", "mrt_renderer_set_max_frames",
     "mrt_accel_create", "mrt_accel_rebuild", "mrt_accel_intersect", "mrt_accel_info_get", "mrt_accel_destroy",
+    "mrt_comm_unique_id", "mrt_comm_create", "mrt_comm_destroy", "mrt_renderer_exchange",
+    "mrt_renderer_exchange_flush", "mrt_renderer_tiles_read", "mrt_renderer_tiles_write",
 ]
 
 _lib = None
@@ -187,6 +193,13 @@ def lib() -> ctypes.CDLL:
         "mrt_accel_intersect": [vp, vp, u32, u32, vp, u32, vp],
         "mrt_accel_info_get": [vp, ctypes.POINTER(AccelInfo)],
         "mrt_accel_destroy": [vp],
+        "mrt_comm_unique_id": [vp, ctypes.c_size_t],
+        "mrt_comm_create": [vp, u32, u32, c_int, ctypes.POINTER(vp)],
+        "mrt_comm_destroy": [vp],
+        "mrt_renderer_exchange": [vp, vp, u32],
+        "mrt_renderer_exchange_flush": [vp],
+        "mrt_renderer_tiles_read": [vp, vp, ctypes.c_size_t],
+        "mrt_renderer_tiles_write": [vp, u32, vp, ctypes.c_size_t],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -365,6 +378,30 @@ class Renderer:
     # -saveCurrentImage
     def save_current_image(self, path: str) -> None:
         _check(lib().mrt_renderer_save_image(self._h, path.encode()), "mrt_renderer_save_image")
+
+    # ---- multi-GPU exchange (include/mrt.h: mrt_renderer_exchange) ----
+    def exchange(self, comm: "Comm", mode: int = EXCHANGE_GATHER) -> None:
+        """Enqueue the image exchange of this shard renderer on its stream:
+        RCCL gather of the packed owned tiles to rank 0 (or SUM reduce)."""
+        _check(lib().mrt_renderer_exchange(self._h, comm.handle, mode), "mrt_renderer_exchange")
+
+    def exchange_flush(self) -> None:
+        _check(lib().mrt_renderer_exchange_flush(self._h), "mrt_renderer_exchange_flush")
+
+    def tiles_read(self, rank: int, count: int):
+        """This shard's owned tiles packed into host memory (float32)."""
+        import numpy as np
+        out = np.zeros(tiles_packed_floats(self.width, self.height, rank, count), np.float32)
+        _check(lib().mrt_renderer_tiles_read(self._h, ctypes.c_void_p(out.ctypes.data), out.size),
+               "mrt_renderer_tiles_read")
+        return out
+
+    def tiles_write(self, shard_rank: int, packed) -> None:
+        """Write another shard's packed tiles (host float32) into the image."""
+        import numpy as np
+        packed = np.ascontiguousarray(packed, np.float32)
+        _check(lib().mrt_renderer_tiles_write(self._h, shard_rank, ctypes.c_void_p(packed.ctypes.data), packed.size),
+               "mrt_renderer_tiles_write")
 
     def stats(self) -> dict:
         s = Stats()
@@ -545,6 +582,42 @@ class Event:
         if self._e.value:
             _check(lib().mrt_event_destroy(self._e), "mrt_event_destroy")
             self._e = ctypes.c_void_p()
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId on rank 0; distribute the bytes to every rank."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().mrt_comm_unique_id(buf, COMM_ID_BYTES), "mrt_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """RCCL communicator of one rank (one process per GPU)."""
+
+    def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int = 0):
+        self._h = None
+        if len(unique_id) != COMM_ID_BYTES:
+            raise MrtError("unique id must be 128 bytes")
+        h = ctypes.c_void_p()
+        _check(lib().mrt_comm_create(ctypes.create_string_buffer(unique_id, COMM_ID_BYTES), nranks, rank, device,
+                                     ctypes.byref(h)), "mrt_comm_create")
+        self._h = h
+        self.nranks, self.rank = nranks, rank
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().mrt_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def device_count() -> int:

@@ -1,0 +1,111 @@
+"""GPU: the multi-GPU exchange of the accumulation image through the C ABI
+(include/mrt.h mrt_comm_* / mrt_renderer_exchange).
+
+One MI355X is available to the tests, so:
+* libmrt's RCCL path runs with a 1-rank communicator: the gather (packed
+  owned tiles -> rank 0 -> unpack), its overlapped form (collective on the
+  communicator's stream, unpack deferred to the next exchange / flush,
+  double-buffered packed tiles ordered by events) and the in-place SUM
+  reduce must leave the 1-GPU image bitwise unchanged, over several steps;
+* the whole N > 1 bench path (tile shards, exchange, max-over-ranks timing,
+  --check-image: rank 0's exchanged image == a 1-GPU render, bitwise) runs
+  as 2 and 3 ranks sharing the GPU, with the host transport (packed tiles to
+  host memory, gloo gather, mrt_renderer_tiles_write on rank 0) — RCCL
+  refuses two ranks on one device.
+The per-rank renders themselves are pinned by the shard-invariance tests."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _render(mrt_mod, sc, W, H, L, frames, steps, comm=None, mode=0, shard=(0, 1)):
+    r = mrt_mod.Renderer(sc, W, H, L, shard_rank=shard[0], shard_count=shard[1])
+    for _ in range(steps):
+        r.reset()
+        r.draw(frames)
+        if comm is not None:
+            r.exchange(comm, mode)
+    img = r.read_image()   # flushes a deferred exchange first
+    r.close()
+    return img
+
+
+@pytest.mark.parametrize("mode", ["gather", "gather_overlap", "reduce"])
+def test_rccl_exchange_single_rank(gpu, mrt_mod, mode):
+    sc = mrt_mod.Scene("cornellbox")
+    W, H, L, frames = 200, 136, 4, 3
+    ref = _render(mrt_mod, sc, W, H, L, frames, 1)
+    comm = mrt_mod.Comm(mrt_mod.comm_unique_id(), 1, 0, 0)
+    m = {"gather": mrt_mod.EXCHANGE_GATHER, "gather_overlap": mrt_mod.EXCHANGE_GATHER | mrt_mod.EXCHANGE_OVERLAP,
+         "reduce": mrt_mod.EXCHANGE_REDUCE}[mode]
+    got = _render(mrt_mod, sc, W, H, L, frames, 3, comm, m)
+    comm.close()
+    assert np.isfinite(ref).all() and ref[..., :3].max() > 0
+    assert got.tobytes() == ref.tobytes()
+
+
+def test_exchange_argument_checks(gpu, mrt_mod):
+    sc = mrt_mod.Scene("cornellbox")
+    comm = mrt_mod.Comm(mrt_mod.comm_unique_id(), 1, 0, 0)
+    r = mrt_mod.Renderer(sc, 64, 64, 2, shard_rank=1, shard_count=2)
+    with pytest.raises(mrt_mod.MrtError, match="shard"):
+        r.exchange(comm, mrt_mod.EXCHANGE_GATHER)   # renderer shard != comm rank/size
+    r.close()
+    r = mrt_mod.Renderer(sc, 64, 64, 2)
+    with pytest.raises(mrt_mod.MrtError, match="mode"):
+        r.exchange(comm, mrt_mod.EXCHANGE_REDUCE | mrt_mod.EXCHANGE_OVERLAP)
+    with pytest.raises(mrt_mod.MrtError, match="mode"):
+        r.exchange(comm, 7)
+    r.close()
+    comm.close()
+
+
+def test_host_tiles_roundtrip(gpu, mrt_mod):
+    """mrt_renderer_tiles_read of every shard renderer, written into one
+    renderer with mrt_renderer_tiles_write, rebuilds the 1-GPU image."""
+    sc = mrt_mod.Scene("cornellbox")
+    W, H, L, frames, S = 300, 170, 3, 2, 3
+    ref = _render(mrt_mod, sc, W, H, L, frames, 1)
+    r0 = mrt_mod.Renderer(sc, W, H, L, shard_rank=0, shard_count=S)
+    r0.draw(frames)
+    for k in range(1, S):
+        rk = mrt_mod.Renderer(sc, W, H, L, shard_rank=k, shard_count=S)
+        rk.draw(frames)
+        packed = rk.tiles_read(k, S)
+        assert packed.size == mrt_mod.tiles_packed_floats(W, H, k, S)
+        rk.close()
+        r0.tiles_write(k, packed)
+    got = r0.read_image()
+    r0.close()
+    assert got[..., :3].tobytes() == ref[..., :3].tobytes()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_multirank_rehearsal(gpu, world):
+    """bench.py's N > 1 path, world ranks on the one GPU (host transport),
+    --check-image asserts rank 0's exchanged image is the 1-GPU render."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--exchange-backend", "host", "--check-image"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == world and d["image_check"] == "bitwise equal to the 1-GPU render"
+    assert d["value"] > 0

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(mrt_mod):
     missing = [n for n in sorted(declared) if not hasattr(lib, n)]
     assert not missing, missing
     assert set(mrt_mod.EXPORTED) == declared
-    assert mrt_mod.lib().mrt_abi_version() == 3
+    assert mrt_mod.lib().mrt_abi_version() == 4
 
 
 def test_device_count_never_fails(mrt_mod):
@@ -150,3 +150,20 @@ def test_accel_argument_errors(mrt_mod):
     assert L.mrt_accel_intersect(None, None, 80, 0, None, 0, None) == -1
     with pytest.raises(mrt_mod.MrtError, match="needs a device"):
         mrt_mod.Scene("cornellbox", device=-1, bvh_builder=mrt_mod.BVH_DEVICE_LBVH)
+
+
+def test_comm_argument_errors_without_device(mrt_mod):
+    """The exchange ABI rejects bad arguments with a status code (no device needed)."""
+    import ctypes
+    L = mrt_mod.lib()
+    h = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(128)
+    assert L.mrt_comm_create(uid, 0, 0, 0, ctypes.byref(h)) == -1     # no ranks
+    assert L.mrt_comm_create(uid, 2, 2, 0, ctypes.byref(h)) == -1     # rank out of range
+    assert L.mrt_comm_create(None, 1, 0, 0, ctypes.byref(h)) == -1
+    assert L.mrt_comm_unique_id(uid, 16) == -1                          # buffer too small
+    assert L.mrt_renderer_exchange(None, None, 1) == -1
+    assert L.mrt_renderer_exchange_flush(None) == -1
+    assert L.mrt_renderer_tiles_read(None, None, 0) == -1
+    assert L.mrt_comm_destroy(None) == 0
+    assert b"bad argument" in L.mrt_last_error() or b"null" in L.mrt_last_error()
