@@ -267,6 +267,7 @@ struct LdsCtx {
   uint32_t stack_base;    // uint32 offset of this lane's stack slot 0
   uint32_t* spill;        // stack entries >= STACK: this lane's column of a global
   uint32_t spill_stride;  //   [entry][lane] spill area (null when STACK covers the BVH)
+  uint32_t spill_hi;      // BVH8 (two-word entries): offset of the second word's plane in the spill area
 };
 
 __device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
@@ -390,7 +391,7 @@ __device__ __forceinline__ int32_t stack_get(const LdsCtx& cx, int sp) {
 template <int MODE>
 __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scratch_u32, uint32_t* spill = nullptr) {
   LdsCtx cx;
-  const uint32_t nf4 = 2 * sc.width;   // float4s per node
+  const uint32_t nf4 = node_float4s(sc.width);   // float4s per node
   const uint32_t n_nodes = (MODE == kAllLds) ? sc.num_nodes : (MODE == kTopLds ? sc.lds_nodes : 0u);
   const uint32_t T = (MODE == kAllLds) ? sc.num_triangles : 0u;
   const uint32_t M = (MODE == kAllLds) ? sc.num_materials : 0u;
@@ -407,6 +408,7 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   cx.stack_base = cx.scratch_base + ((scratch_u32 + 3) & ~3u) + threadIdx.x;
   cx.spill_stride = gridDim.x * kBlock;
   cx.spill = spill ? spill + blockIdx.x * kBlock + threadIdx.x : nullptr;
+  cx.spill_hi = sc.max_stack * cx.spill_stride;
   if (MODE != kGlobal) {
     const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes), reinterpret_cast<const float4*>(sc.tris),
                             reinterpret_cast<const float4*>(sc.prims), reinterpret_cast<const float4*>(sc.materials),
@@ -547,6 +549,188 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
   return false;
 }
 
+
+// ---------------------------------------------------------------------------
+// Compressed BVH8 traversal (node layout in mrt_layout.h), for scenes whose
+// nodes live in global memory (top levels staged in LDS).  Stack entries are
+// groups, two words each ([entry][lane] planes in LDS, spilling to global):
+//   node group     (base node, pending children in visiting order | imask << 8)
+//   triangle group (first triangle, pending triangle bits | 1 << 31)
+// A lane descends interior nodes while it holds at most one parked triangle
+// group (postponing, as in the BVH4 walk) until every lane of the wave holds
+// one; then the wave tests triangles.  Child visiting order: slot (k ^ ray
+// octant) k-th, no sorting.  Nearest / any-hit answers are order independent.
+// ---------------------------------------------------------------------------
+template <int STACK>
+__device__ __forceinline__ void stack_push2(const LdsCtx& cx, int sp, uint32_t lo, uint32_t hi) {
+  constexpr int kL = STACK < 0 ? -STACK : STACK;
+  if (STACK > 0 || sp < kL) {
+    lds_u32()[cx.stack_base + sp * kBlock] = lo;
+    lds_u32()[cx.stack_base + (kL + sp) * kBlock] = hi;
+  } else {
+    cx.spill[(size_t)(sp - kL) * cx.spill_stride] = lo;
+    cx.spill[(size_t)(sp - kL) * cx.spill_stride + cx.spill_hi] = hi;
+  }
+}
+template <int STACK>
+__device__ __forceinline__ void stack_get2(const LdsCtx& cx, int sp, uint32_t& lo, uint32_t& hi) {
+  constexpr int kL = STACK < 0 ? -STACK : STACK;
+  if (STACK > 0 || sp < kL) {
+    lo = lds_u32()[cx.stack_base + sp * kBlock];
+    hi = lds_u32()[cx.stack_base + (kL + sp) * kBlock];
+  } else {
+    lo = cx.spill[(size_t)(sp - kL) * cx.spill_stride];
+    hi = cx.spill[(size_t)(sp - kL) * cx.spill_stride + cx.spill_hi];
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void fetch_node8(const DeviceScene& sc, const LdsCtx& cx, uint32_t node, float4 q[5]) {
+  if (MODE == kAllLds || (MODE == kTopLds && node < cx.n_lds_nodes)) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) q[i] = g_lds[5 * node + i];
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 5 * (size_t)node;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) q[i] = p[i];
+  }
+}
+
+// permute the 8 slot bits of x so bit (s ^ oct) holds slot s
+__device__ __forceinline__ uint32_t octant_order(uint32_t x, uint32_t oct) {
+  x = (oct & 1u) ? (((x & 0x55u) << 1) | ((x >> 1) & 0x55u)) : x;
+  x = (oct & 2u) ? (((x & 0x33u) << 2) | ((x >> 2) & 0x33u)) : x;
+  x = (oct & 4u) ? (((x & 0x0Fu) << 4) | ((x >> 4) & 0x0Fu)) : x;
+  return x;
+}
+
+// slab entry distance of quantised plane q on one axis (see mrt_layout.h):
+// precise: ((p + 2^e q) - o) * inv, the plane exactly as the builder checked it;
+// fast: fma(q, 2^e inv, (p - o) inv)
+struct Axis8 { float p, s, o, inv, sinv, base; };
+__device__ __forceinline__ float qslab(float qf, const Axis8& a) {
+#if MRT_PRECISE
+  return ((a.p + a.s * qf) - a.o) * a.inv;
+#else
+  return fmaf(qf, a.sinv, a.base);
+#endif
+}
+
+// Test the 8 children of a node: returns the hit slot mask; tri_bits gets the
+// triangle bits of the hit leaf slots (relative to the node's tri_base).
+__device__ __forceinline__ uint32_t box8(const float4 q[5], V3 o, const RayBox& rb, float tmin, float tmax,
+                                         uint32_t& tri_bits) {
+  const uint32_t ew = fbits(q[0].w);
+  Axis8 ax[3];
+  const float pp[3] = {q[0].x, q[0].y, q[0].z}, oo[3] = {o.x, o.y, o.z}, iv[3] = {rb.inv.x, rb.inv.y, rb.inv.z};
+#if !MRT_PRECISE
+  const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
+#endif
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    ax[a].p = pp[a];
+    ax[a].o = oo[a];
+    ax[a].inv = iv[a];
+    ax[a].s = bitsf((((ew >> (8 * a)) & 0xFFu) - 1u) << 23);   // 2^(byte - 128)
+#if !MRT_PRECISE
+    ax[a].sinv = ax[a].s * iv[a];
+    ax[a].base = fmaf(pp[a], iv[a], -oi[a]);
+#endif
+  }
+  // near / far byte planes by the direction's signs (inv < 0: the hi plane is near)
+  const uint32_t sx = fbits(rb.inv.x) >> 31, sy = fbits(rb.inv.y) >> 31, sz = fbits(rb.inv.z) >> 31;
+  const uint32_t lx0 = fbits(q[2].x), lx1 = fbits(q[2].y), ly0 = fbits(q[2].z), ly1 = fbits(q[2].w);
+  const uint32_t lz0 = fbits(q[3].x), lz1 = fbits(q[3].y), hx0 = fbits(q[3].z), hx1 = fbits(q[3].w);
+  const uint32_t hy0 = fbits(q[4].x), hy1 = fbits(q[4].y), hz0 = fbits(q[4].z), hz1 = fbits(q[4].w);
+  const uint32_t nx[2] = {sx ? hx0 : lx0, sx ? hx1 : lx1}, fx[2] = {sx ? lx0 : hx0, sx ? lx1 : hx1};
+  const uint32_t ny[2] = {sy ? hy0 : ly0, sy ? hy1 : ly1}, fy[2] = {sy ? ly0 : hy0, sy ? ly1 : hy1};
+  const uint32_t nz[2] = {sz ? hz0 : lz0, sz ? hz1 : lz1}, fz[2] = {sz ? lz0 : hz0, sz ? lz1 : hz1};
+  const uint32_t meta[2] = {fbits(q[1].z), fbits(q[1].w)};
+  uint32_t hits = 0, tb = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int w = c >> 2, sh = 8 * (c & 3);
+    const float tnx = qslab((float)((nx[w] >> sh) & 0xFFu), ax[0]), tfx = qslab((float)((fx[w] >> sh) & 0xFFu), ax[0]);
+    const float tny = qslab((float)((ny[w] >> sh) & 0xFFu), ax[1]), tfy = qslab((float)((fy[w] >> sh) & 0xFFu), ax[1]);
+    const float tnz = qslab((float)((nz[w] >> sh) & 0xFFu), ax[2]), tfz = qslab((float)((fz[w] >> sh) & 0xFFu), ax[2]);
+    const float tnear = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+    const float tfar = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
+    const bool hit = tnear <= tfar;
+    const uint32_t m = (meta[w] >> sh) & 0xFFu;
+    hits |= hit ? (1u << c) : 0u;
+    tb |= hit ? ((m >> 5) << (m & 31u)) : 0u;
+  }
+  tri_bits = tb;
+  return hits;
+}
+
+template <int STACK, int MODE, bool ANY>
+__device__ __forceinline__ bool traverse8(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
+                                          uint32_t target) {
+  const RayBox rb = make_raybox(o, d);
+  const uint32_t oct = (fbits(rb.inv.x) >> 31) | ((fbits(rb.inv.y) >> 31) << 1) | ((fbits(rb.inv.z) >> 31) << 2);
+  uint32_t gbase = (uint32_t)sc.root, gbits = 1u;   // the root: one pending child at rank 0 (imask 0)
+  uint32_t tbase = 0, tbits = 0;                    // parked triangle group
+  int sp = 0;
+  while ((gbits & 0xFFu) | tbits | (uint32_t)sp) {
+    // interior nodes
+    for (;;) {
+      if ((gbits & 0xFFu) == 0) {
+        if (sp == 0) break;
+        uint32_t lo, hi;
+        stack_get2<STACK>(cx, sp - 1, lo, hi);
+        if (hi >> 31) {                 // a postponed triangle group
+          if (tbits) break;             //   one is parked already: test that first
+          tbase = lo;
+          tbits = hi & 0x00FFFFFFu;
+          --sp;
+          break;
+        }
+        gbase = lo;
+        gbits = hi;
+        --sp;
+      }
+      const uint32_t k = __builtin_ctz(gbits & 0xFFu);
+      gbits &= gbits - 1u;              // the low byte is non-zero: clears bit k
+      const uint32_t slot = k ^ oct;
+      const uint32_t node = gbase + __popc((gbits >> 8) & ((1u << slot) - 1u));
+      if (gbits & 0xFFu) { stack_push2<STACK>(cx, sp, gbase, gbits); ++sp; }
+      float4 q[5];
+      fetch_node8<MODE>(sc, cx, node, q);
+      uint32_t tb;
+      const uint32_t hitm = box8(q, o, rb, tmin, h.t, tb);
+      const uint32_t imask = fbits(q[0].w) >> 24;
+      gbase = fbits(q[1].x);
+      gbits = octant_order(hitm & imask, oct) | (imask << 8);
+      if (tb) {
+        if (tbits) { stack_push2<STACK>(cx, sp, fbits(q[1].y), tb | 0x80000000u); ++sp; }
+        else { tbase = fbits(q[1].y); tbits = tb; }
+      }
+      if (!__any(tbits == 0)) break;    // every lane still descending holds triangles
+    }
+    // triangles of the parked group
+    while (tbits) {
+      const uint32_t k = __builtin_ctz(tbits);
+      tbits &= tbits - 1u;
+      float4 t0, t1, t2;
+      fetch_tri<MODE>(sc, cx, tbase + k, t0, t1, t2);
+      const uint32_t prim = fbits(t0.w);
+      float t, u, v;
+      const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v);
+      if (ANY) {
+        if (hit & (prim != target) & ((t < h.t) | (prim < target))) return true;
+      } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
+        h.found = true;
+        h.t = t;
+        h.u = u;
+        h.v = v;
+        h.prim = prim;
+      }
+    }
+  }
+  return false;
+}
+
 template <int STACK, int MODE, int WIDTH>
 __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
                                              float tmax) {
@@ -555,7 +739,8 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
-  traverse<STACK, MODE, WIDTH, false>(sc, cx, o, d, tmin, h, 0u);
+  if constexpr (WIDTH == 8) traverse8<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u);
+  else traverse<STACK, MODE, WIDTH, false>(sc, cx, o, d, tmin, h, 0u);
   return h;
 }
 
@@ -565,7 +750,8 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
   Hit h;
   h.t = t_target;
   h.found = false;
-  return traverse<STACK, MODE, WIDTH, true>(sc, cx, o, d, 0.0f, h, target);
+  if constexpr (WIDTH == 8) return traverse8<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target);
+  else return traverse<STACK, MODE, WIDTH, true>(sc, cx, o, d, 0.0f, h, target);
 }
 
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
@@ -1354,17 +1540,18 @@ int choose_mode(const DeviceScene& sc) {
     return v ? std::atoi(v) : -1;
   }();
   if (forced >= 0 && forced <= 2) return forced;
-  if ((size_t)lds_scene_float4s(kAllLds, 2 * sc.width, sc.num_nodes, 0, sc.num_triangles, sc.num_materials,
+  if ((size_t)lds_scene_float4s(kAllLds, node_float4s(sc.width), sc.num_nodes, 0, sc.num_triangles, sc.num_materials,
                                 sc.num_lights + 1) * 16 <= kAllLdsBudget)
     return kAllLds;
   return sc.lds_nodes > 0 ? kTopLds : kGlobal;
 }
 
 size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
-  const size_t scene = (size_t)lds_scene_float4s(mode, 2 * sc.width, sc.num_nodes, sc.lds_nodes, sc.num_triangles,
-                                                 sc.num_materials, sc.num_lights + 1) * 16;
+  const size_t scene = (size_t)lds_scene_float4s(mode, node_float4s(sc.width), sc.num_nodes, sc.lds_nodes,
+                                                 sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16;
   const size_t scratch = ((size_t)2 * grid + 1 + 3) / 4 * 16;   // 2 segments per block + sentinel
-  return scene + scratch + (size_t)stack * kBlock * 4;   // stack = LDS entries (|STACK|)
+  const size_t entry_words = sc.width == 8 ? 2 : 1;              // BVH8: two-word group entries
+  return scene + scratch + (size_t)stack * entry_words * kBlock * 4;   // stack = LDS entries (|STACK|)
 }
 
 // kTopLds: stage only as many top BVH nodes as keep the block's LDS within
@@ -1381,7 +1568,7 @@ DeviceScene fit_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack, uint3
   if (mode != kTopLds) return sc;
   DeviceScene f = sc;
   const size_t fixed = bounce_lds_bytes(sc, kGlobal, stack, grid) + 64;   // scratch + stack + static
-  const size_t node_bytes = (size_t)sc.width * 32;
+  const size_t node_bytes = (size_t)node_float4s(sc.width) * 16;
   const size_t fit = fixed < kLdsPerBlockTarget ? (kLdsPerBlockTarget - fixed) / node_bytes : 0;
   f.lds_nodes = (uint32_t)std::min<size_t>(sc.lds_nodes, fit);
   return f;
@@ -1440,6 +1627,7 @@ hipError_t dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32_t gr
 template <int STACK>
 hipError_t dispatch_width(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
                           hipStream_t s) {
+  if (sc.width == 8) return dispatch_mode<STACK, 8>(sc, a, grid, grid_out, s);
   return sc.width == 4 ? dispatch_mode<STACK, 4>(sc, a, grid, grid_out, s)
                        : dispatch_mode<STACK, 2>(sc, a, grid, grid_out, s);
 }
@@ -1472,6 +1660,12 @@ hipError_t launch_intersect(const DeviceScene& sc, const void* rays, uint32_t st
                             RefIntersection* out, uint32_t* spill, hipStream_t s) {
   if (count == 0) return hipSuccess;
   const uint8_t* r = reinterpret_cast<const uint8_t*>(rays);
+  if (sc.width == 8) {   // BVH8: <= 32 levels (one group entry per level), two words per entry in LDS
+    if (sc.max_stack > 32) return hipErrorInvalidValue;
+    const size_t lds = (size_t)32 * 2 * kBlock * 4;
+    intersect_kernel<8, 32><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);
+    return hipGetLastError();
+  }
   if (sc.max_stack <= (uint32_t)kMaxStack) {   // whole stack in LDS
     const size_t lds = (size_t)kMaxStack * kBlock * 4;
     if (sc.width == 4) intersect_kernel<4, kMaxStack><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);

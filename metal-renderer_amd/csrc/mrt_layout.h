@@ -73,6 +73,26 @@ static_assert(sizeof(RefLightTriangle) == 100, "RefLightTriangle");
 //   [4] = lo.z[0..3]  [5] = hi.z[0..3]  [6] = bits(ref[0..3])  [7] = 0
 // Unused child slots carry ref == kEmptyChild (and a zero box); the traversal
 // masks them by ref, never by box.
+//
+// BVH8 node i = nodes[5i .. 5i+4] (80 B): compressed 8-wide node, for scenes
+// traversed from global memory (compressed wide BVH after Ylitie, Karras &
+// Laine, HPG 2017, with our own encoding):
+//   [0] = (p.x, p.y, p.z, bits(ex | ey << 8 | ez << 16 | imask << 24))
+//         p = quantisation origin, e* = per-axis exponent + 128 (scale 2^e),
+//         imask bit s = slot s holds an interior child
+//   [1] = (bits(child_base), bits(tri_base), bits(meta[0..3]), bits(meta[4..7]))
+//         interior child in slot s = node child_base + popcount(imask & ((1 << s) - 1));
+//         meta[s] of a leaf slot = (unary triangle count (1, 3, 7) << 5) | offset:
+//         triangles tri_base + offset .. (count <= 3, offset + count <= 24); 0 otherwise
+//   [2] = qlo.x[0..7], qlo.y[0..7]   (one byte per slot)
+//   [3] = qlo.z[0..7], qhi.x[0..7]
+//   [4] = qhi.y[0..7], qhi.z[0..7]
+// Child box = p + 2^e * q (exact product, one rounding in the add), rounded
+// outward at build time and checked in float, so the slab test stays
+// conservative.  Empty slots have qlo = 255 > qhi = 0 and no imask/meta bits.
+// Slots follow the octant of the child's centroid relative to the node
+// centre: a ray in octant o (bit a set where direction a < 0) visits slot
+// (k ^ o) k-th, an approximately near-to-far order without sorting.
 constexpr int32_t kEmptyChild = 0x7FFFFFFF;
 constexpr int kLeafCountBits = 4;
 constexpr int kMaxLeafSize = 1 << kLeafCountBits;   // 16
@@ -100,8 +120,16 @@ struct DeviceScene {
   uint32_t num_materials;
   uint32_t num_lights;       // light triangles, excluding the sentinel (SharedData.lightTrianglesCount)
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
-  uint32_t width;            // 2 = BVH2, 4 = BVH4
+  uint32_t width;            // 2 = BVH2, 4 = BVH4, 8 = compressed BVH8
   uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack)
 };
+
+// float4s per node record of a BVH width
+#if defined(__HIPCC__)
+#define MRT_HD __host__ __device__
+#else
+#define MRT_HD
+#endif
+MRT_HD constexpr uint32_t node_float4s(uint32_t width) { return width == 8 ? 5u : 2u * width; }
 
 }  // namespace mrt

@@ -288,8 +288,10 @@ int alloc_frame_buffers(mrt_renderer* r) {
       for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(slots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
-    if (need > r->stack_entries && !fs.spill.p)
-      HIP_TRY(fs.spill.alloc((size_t)(need - r->stack_entries) * r->grid * 256 * 4));
+    // BVH8 group entries are two words: the second plane starts max_stack
+    // entries into the area (kernels.hip LdsCtx::spill_hi)
+    const size_t spill_entries = r->scene->dev.width == 8 ? 2 * (size_t)need : (size_t)(need - r->stack_entries);
+    if (need > r->stack_entries && !fs.spill.p) HIP_TRY(fs.spill.alloc(spill_entries * r->grid * 256 * 4));
   }
   if (r->own_image) {
     if (r->image) (void)hipFree(r->image);
@@ -570,10 +572,14 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (const char* v = std::getenv("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
   if (const char* v = std::getenv("MRT_BINS")) opt.bins = (uint32_t)std::strtoul(v, nullptr, 0);
   if (const char* v = std::getenv("MRT_EXACT_SAH")) opt.exact_sah_below = (uint32_t)std::strtoul(v, nullptr, 0);
-  opt.width = desc->bvh_width ? desc->bvh_width : 4;
-  if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
-  if (opt.width != 2 && opt.width != 4) return fail(MRT_ERR_INVALID, "bvh_width must be 2 or 4");
   const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
+  // default width: BVH4 for scenes small enough to be staged whole in LDS
+  // (quadrant-copy nodes, kernels.hip kAllLds), the compressed BVH8 for
+  // scenes traversed from global memory; the device builders emit BVH4
+  opt.width = desc->bvh_width ? desc->bvh_width : (builder != MRT_BVH_HOST_SAH || T <= 256 ? 4 : 8);
+  if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (opt.width != 2 && opt.width != 4 && opt.width != 8) return fail(MRT_ERR_INVALID, "bvh_width must be 2, 4 or 8");
+  if (opt.width == 8 && opt.max_leaf_size > 3) opt.max_leaf_size = 3;   // BVH8 leaf slots hold <= 3 triangles
   if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH && builder != MRT_BVH_DEVICE_PLOC)
     return fail(MRT_ERR_INVALID, "unknown bvh_builder");
   if (builder != MRT_BVH_HOST_SAH && desc->device < 0) return fail(MRT_ERR_INVALID, "device BVH build needs a device");
@@ -715,10 +721,79 @@ int mrt_scene_export(const mrt_scene* scene, void* vertices, void* indices, void
   return MRT_OK;
 }
 
+namespace {
+// Structural check of a compressed BVH8 (mrt_layout.h): every node reachable
+// once, every child box (dequantised exactly as the kernels do) inside its
+// parent's and containing its subtree's triangles, every primitive in one
+// leaf slot with the right record, stack bound = levels.
+int check_bvh8(const mrt::BvhResult& b, const mrt::HostScene& h) {
+  const uint32_t T = (uint32_t)h.references.size();
+  std::vector<uint8_t> seen(T, 0), node_seen(b.num_nodes, 0);
+  auto fb = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+  struct Item { uint32_t node, level; float lo[3], hi[3]; };
+  std::vector<Item> st{{0u, 0u, {-1e30f, -1e30f, -1e30f}, {1e30f, 1e30f, 1e30f}}};
+  while (!st.empty()) {
+    const Item it = st.back();
+    st.pop_back();
+    if (it.node >= b.num_nodes || node_seen[it.node]) return fail(MRT_ERR_STATE, "BVH8 node out of range or reached twice");
+    node_seen[it.node] = 1;
+    if (it.level >= b.max_stack) return fail(MRT_ERR_STATE, "BVH8 stack bound too small");
+    const float* n = &b.nodes[20 * (size_t)it.node];
+    const uint32_t ew = fb(n[3]), imask = ew >> 24, child_base = fb(n[4]), tri_base = fb(n[5]);
+    const uint32_t meta[2] = {fb(n[6]), fb(n[7])};
+    uint32_t rank = 0;
+    for (uint32_t s = 0; s < 8; ++s) {
+      const uint32_t m = (meta[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+      const bool internal = (imask >> s) & 1u;
+      if (!internal && m == 0) continue;
+      if (internal && m) return fail(MRT_ERR_STATE, "BVH8 slot both interior and leaf");
+      float lo[3], hi[3];
+      for (int a = 0; a < 3; ++a) {
+        const int e = (int)((ew >> (8 * a)) & 0xFFu) - 128;
+        const uint32_t w = 8 + 2 * a + (s >> 2), wh = 14 + 2 * a + (s >> 2);
+        const uint32_t ql = (fb(n[w]) >> (8 * (s & 3))) & 0xFFu, qh = (fb(n[wh]) >> (8 * (s & 3))) & 0xFFu;
+        lo[a] = n[a] + std::ldexp((float)ql, e);
+        hi[a] = n[a] + std::ldexp((float)qh, e);
+        if (!(lo[a] <= hi[a])) return fail(MRT_ERR_STATE, "BVH8 empty child box");
+      }
+      if (internal) {
+        st.push_back({child_base + rank++, it.level + 1, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
+        continue;
+      }
+      const uint32_t off = m & 31u, unary = m >> 5;
+      const uint32_t cnt = unary == 1 ? 1 : unary == 3 ? 2 : unary == 7 ? 3 : 0;
+      if (!cnt || off + cnt > 24 || tri_base + off + cnt > T) return fail(MRT_ERR_STATE, "BVH8 bad leaf slot");
+      for (uint32_t k = tri_base + off; k < tri_base + off + cnt; ++k) {
+        const float* t = &b.tris[12 * (size_t)k];
+        const uint32_t prim = fb(t[3]);
+        if (prim >= T || seen[prim]) return fail(MRT_ERR_STATE, "BVH primitive missing or duplicated");
+        seen[prim] = 1;
+        const float* v[3] = {h.vertices[h.references[prim].tri[0]].v, h.vertices[h.references[prim].tri[1]].v,
+                             h.vertices[h.references[prim].tri[2]].v};
+        for (int c = 0; c < 3; ++c)
+          for (int a = 0; a < 3; ++a)
+            if (!(v[c][a] >= lo[a] && v[c][a] <= hi[a])) return fail(MRT_ERR_STATE, "BVH box does not contain its triangle");
+        for (int a = 0; a < 3; ++a)
+          if (t[a] != v[0][a] || t[4 + a] != v[1][a] - v[0][a] || t[8 + a] != v[2][a] - v[0][a])
+            return fail(MRT_ERR_STATE, "BVH leaf triangle record mismatch");
+      }
+    }
+    if (rank != (uint32_t)__builtin_popcount(imask)) return fail(MRT_ERR_STATE, "BVH8 interior child count");
+    (void)it.lo;
+  }
+  for (uint32_t t = 0; t < T; ++t)
+    if (!seen[t]) return fail(MRT_ERR_STATE, "BVH primitive not referenced");
+  for (uint32_t k = 0; k < b.num_nodes; ++k)
+    if (!node_seen[k]) return fail(MRT_ERR_STATE, "BVH has unreachable nodes");
+  return MRT_OK;
+}
+}  // namespace
+
 int mrt_scene_check_bvh(const mrt_scene* scene) {
   if (!scene) return fail(MRT_ERR_INVALID, "null scene");
   const mrt::BvhResult& b = scene->bvh;
   const mrt::HostScene& h = scene->host;
+  if (b.width == 8) return check_bvh8(b, h);
   const uint32_t T = (uint32_t)h.references.size();
   std::vector<uint8_t> seen(T, 0);
   auto fbits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };

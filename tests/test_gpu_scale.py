@@ -17,7 +17,7 @@ from helpers import SEED, compare_to_golden, dev_ptr, from_dev, pixel_metrics, t
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[2, 4], ids=["bvh2", "bvh4"])
+@pytest.fixture(scope="module", params=[2, 4, 8], ids=["bvh2", "bvh4", "bvh8"])
 def proc_scenes(request, gpu, mrt_mod, oracle_mod):
     """cornellbox + an 8192-triangle procedural sphere, product and oracle
     built from the same flattened buffers."""
