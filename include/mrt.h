@@ -237,6 +237,21 @@ int mrt_shard_mask(uint32_t width, uint32_t height, uint32_t shard_rank, uint32_
 int mrt_display(const float* image, const float* reference, float* out, uint32_t width, uint32_t height,
                 uint32_t flags, float compare_scale, void* stream);
 
+/* Golden images: loadReferenceImage (renderer/Renderer.mm:162-253) reads
+ * Media/reference/<scene>-<L>.exr (Mitsuba goldens: ZIP-compressed half RGB)
+ * and flips it into the comparison texture.  mrt_image_load_exr decodes a
+ * scanline OpenEXR file (NONE / ZIPS / ZIP compression, HALF / FLOAT / UINT
+ * channels; R, G, B, A by name, A = 1 if absent) into host RGBA32F with
+ * row 0 = BOTTOM; call with rgba = NULL to get the size first.  No device. */
+int mrt_image_load_exr(const char* path, float* rgba, size_t capacity_floats, uint32_t* width, uint32_t* height);
+/* The renderer's comparison image (COMPARISON_MODE != 0): the golden at
+ * `path`, which must have the renderer's W x H, uploaded to the device. */
+int mrt_renderer_load_reference(mrt_renderer* r, const char* path);
+/* blitFragment for a host without its own GPU code: mrt_display of the
+ * accumulation image (tone map / sRGB / compare mode against the loaded
+ * reference) into host memory (rgba: W*H*4 floats, row 0 = bottom). */
+int mrt_renderer_display(mrt_renderer* r, uint32_t flags, float compare_scale, float* rgba, size_t count);
+
 /* Multi-GPU exchange of the accumulation image: a shard's
  * owned 64x64 tiles packed densely, [k][64*64] RGBA32F for its k-th owned
  * tile (tile t = shard_rank + k*shard_count, row-major tiles; zeros outside

@@ -26,6 +26,7 @@
 #include "../../include/mrt.h"
 #include "bvh.h"
 #include "bvh_gpu.h"
+#include "image.h"
 #include "kernels.h"
 #include "noise.h"
 #include "scene.h"
@@ -182,6 +183,7 @@ struct mrt_renderer {
   uint32_t stack_entries = 32;
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
   Exchange x;
+  DevBuf reference, display;   // comparison image (mrt_renderer_load_reference) and blit output
 };
 
 namespace {
@@ -1285,6 +1287,50 @@ int mrt_renderer_save_image(mrt_renderer* r, const char* path) {
   if (ends(".pfm")) return write_pfm(path, img, W, H);
   if (ends(".exr")) return write_exr(path, img, W, H);
   return fail(MRT_ERR_INVALID, "unsupported image extension (use .pfm or .exr)");
+}
+
+int mrt_image_load_exr(const char* path, float* rgba, size_t capacity, uint32_t* width, uint32_t* height) {
+  if (!path || !width || !height) return fail(MRT_ERR_INVALID, "mrt_image_load_exr: null argument");
+  std::vector<float> img;
+  uint32_t W = 0, H = 0;
+  std::string err;
+  if (!mrt::load_exr(path, img, W, H, err)) return fail(MRT_ERR_IO, err);
+  *width = W;
+  *height = H;
+  if (!rgba) return MRT_OK;
+  if (capacity < img.size()) return fail(MRT_ERR_INVALID, "mrt_image_load_exr: buffer too small");
+  std::memcpy(rgba, img.data(), img.size() * 4);
+  return MRT_OK;
+}
+
+int mrt_renderer_load_reference(mrt_renderer* r, const char* path) {
+  if (!r || !path) return fail(MRT_ERR_INVALID, "null argument");
+  std::vector<float> img;
+  uint32_t W = 0, H = 0;
+  std::string err;
+  if (!mrt::load_exr(path, img, W, H, err)) return fail(MRT_ERR_IO, err);
+  if (W != r->desc.width || H != r->desc.height)
+    return fail(MRT_ERR_INVALID, "reference image is " + std::to_string(W) + "x" + std::to_string(H) + ", renderer " +
+                                     std::to_string(r->desc.width) + "x" + std::to_string(r->desc.height));
+  HIP_TRY(hipSetDevice(r->scene->device));
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  HIP_TRY(upload(r->reference, img.data(), img.size() * 4));
+  return MRT_OK;
+}
+
+int mrt_renderer_display(mrt_renderer* r, uint32_t flags, float compare_scale, float* rgba, size_t count) {
+  if (!r || !rgba) return fail(MRT_ERR_INVALID, "null argument");
+  const size_t need = (size_t)r->desc.width * r->desc.height * 4;
+  if (count < need) return fail(MRT_ERR_INVALID, "output buffer too small");
+  if (((flags >> 8) & 0xFFu) && !r->reference.p) return fail(MRT_ERR_STATE, "compare mode without a loaded reference");
+  int rc = exchange_flush(r);
+  if (rc) return rc;
+  if (r->display.bytes < need * 4) HIP_TRY(r->display.alloc(need * 4));
+  rc = mrt_display(r->image, r->reference.as<float>(), r->display.as<float>(), r->desc.width, r->desc.height, flags,
+                   compare_scale, r->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(rgba, r->display.p, need * 4, hipMemcpyDeviceToHost, r->stream));
+  return mrt_renderer_sync(r);
 }
 
 int mrt_renderer_stats(const mrt_renderer* r, mrt_stats* stats) {

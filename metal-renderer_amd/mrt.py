@@ -130,6 +130,7 @@ EXPORTED = [
     "mrt_accel_create", "mrt_accel_rebuild", "mrt_accel_intersect", "mrt_accel_info_get", "mrt_accel_destroy",
     "mrt_comm_unique_id", "mrt_comm_create", "mrt_comm_destroy", "mrt_renderer_exchange",
     "mrt_renderer_exchange_flush", "mrt_renderer_tiles_read", "mrt_renderer_tiles_write",
+    "mrt_image_load_exr", "mrt_renderer_load_reference", "mrt_renderer_display",
 ]
 
 _lib = None
@@ -200,6 +201,9 @@ def lib() -> ctypes.CDLL:
         "mrt_renderer_exchange_flush": [vp],
         "mrt_renderer_tiles_read": [vp, vp, ctypes.c_size_t],
         "mrt_renderer_tiles_write": [vp, u32, vp, ctypes.c_size_t],
+        "mrt_image_load_exr": [ctypes.c_char_p, vp, ctypes.c_size_t, ctypes.POINTER(u32), ctypes.POINTER(u32)],
+        "mrt_renderer_load_reference": [vp, ctypes.c_char_p],
+        "mrt_renderer_display": [vp, u32, ctypes.c_float, vp, ctypes.c_size_t],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -403,6 +407,18 @@ class Renderer:
         _check(lib().mrt_renderer_tiles_write(self._h, shard_rank, ctypes.c_void_p(packed.ctypes.data), packed.size),
                "mrt_renderer_tiles_write")
 
+    # ---- golden comparison (loadReferenceImage + blitFragment) ----
+    def load_reference(self, path: str) -> None:
+        _check(lib().mrt_renderer_load_reference(self._h, path.encode()), "mrt_renderer_load_reference")
+
+    def display(self, flags: int = 0, compare_scale: float = 10.0):
+        """[H, W, 4] float32 blit of the image (row 0 = bottom)."""
+        import numpy as np
+        img = np.zeros((self.height, self.width, 4), np.float32)
+        _check(lib().mrt_renderer_display(self._h, flags, compare_scale, ctypes.c_void_p(img.ctypes.data), img.size),
+               "mrt_renderer_display")
+        return img
+
     def stats(self) -> dict:
         s = Stats()
         _check(lib().mrt_renderer_stats(self._h, ctypes.byref(s)), "mrt_renderer_stats")
@@ -582,6 +598,18 @@ class Event:
         if self._e.value:
             _check(lib().mrt_event_destroy(self._e), "mrt_event_destroy")
             self._e = ctypes.c_void_p()
+
+
+def load_exr(path: str):
+    """Decode a scanline OpenEXR file (libmrt's reader): [H, W, 4] float32,
+    row 0 = BOTTOM."""
+    import numpy as np
+    w, h = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().mrt_image_load_exr(path.encode(), None, 0, ctypes.byref(w), ctypes.byref(h)), "mrt_image_load_exr")
+    img = np.zeros((h.value, w.value, 4), np.float32)
+    _check(lib().mrt_image_load_exr(path.encode(), ctypes.c_void_p(img.ctypes.data), img.size, ctypes.byref(w),
+                                    ctypes.byref(h)), "mrt_image_load_exr")
+    return img
 
 
 def comm_unique_id() -> bytes:

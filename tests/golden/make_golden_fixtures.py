@@ -7,6 +7,8 @@ Fixture contents (data only: inputs/expected outputs):
   * per golden: banner-masked mean linear RGB, peak, and a 40x30 block-mean
     image (20x20-pixel blocks of the 800x600 image, row 0 = TOP, banner
     masked to 0 — the same mask is applied to our renders before comparing).
+  * white-box-2.exr: one golden copied unchanged (data; the smallest, 428 KB)
+    as the fixture of libmrt's own EXR reader (tests/test_host.py);
   * the scene OBJ/MTL data files the reference ships (renderer/Media/*.obj,
     *.mtl) are copied unchanged into metal-renderer_amd/scenes/: they are the
     product's input data ("scenes in renderer/Media render unchanged"), not
@@ -63,6 +65,7 @@ def main():
                "CornellBox-Water-plastic.mtl", "CornellBox-Water-mirror.obj", "CornellBox-Water-mirror.mtl",
                "CornellBox-Water.obj", "CornellBox-Water.mtl"):
         shutil.copyfile(os.path.join(REF, fn), os.path.join(sdir, fn))
+    shutil.copyfile(os.path.join(REF, "reference", "white-box-2.exr"), os.path.join(HERE, "white-box-2.exr"))
     print(json.dumps(stats, indent=1))
 
 

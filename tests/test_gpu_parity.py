@@ -315,3 +315,30 @@ def test_pack_on_renderer_stream(gpu, mrt_mod):
     r.close()
     assert np.any(img != 0)
     assert got.tobytes() == mrt_mod.tiles_pack_host(img, 1, count).tobytes()
+
+
+def test_golden_compare_display(gpu, mrt_mod, oracle_mod):
+    """COMPARISON_MODE end to end from the C ABI (Renderer.mm:162-253 +
+    Shaders.metal:53-66): load the reference's white-box-2 golden with
+    libmrt's EXR reader into the renderer, blit each compare mode to host
+    memory, equal to the numpy restatement of blitFragment on the same
+    images."""
+    import os
+    golden_path = os.path.join(os.path.dirname(__file__), "golden", "white-box-2.exr")
+    sc = _scene(mrt_mod, "white-box")
+    r = mrt_mod.Renderer(sc, 800, 600, 2)
+    r.draw(4)
+    img = r.read_image()
+    r.load_reference(golden_path)
+    gold = mrt_mod.load_exr(golden_path)
+    for flags in (0, 1, 3, (1 << 8), (2 << 8) | 1, (3 << 8) | 2, (4 << 8) | 3):
+        got = r.display(flags, 10.0)
+        want = oracle_mod.display(img, gold, flags, 10.0)
+        np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-5)
+    with pytest.raises(mrt_mod.MrtError, match="reference image"):
+        r2 = mrt_mod.Renderer(sc, 64, 48, 2)
+        try:
+            r2.load_reference(golden_path)
+        finally:
+            r2.close()
+    r.close()

@@ -185,3 +185,67 @@ def test_comm_argument_errors_without_device(mrt_mod):
     assert L.mrt_renderer_tiles_read(None, None, 0) == -1
     assert L.mrt_comm_destroy(None) == 0
     assert b"bad argument" in L.mrt_last_error() or b"null" in L.mrt_last_error()
+
+
+def _write_exr(path, rgb, comp, ptype):
+    """Tiny scanline EXR writer (test-only): comp 0 NONE / 2 ZIPS, ptype 1 HALF / 2 FLOAT, B G R channels."""
+    import struct
+    import zlib
+    H, W, _ = rgb.shape
+    out = bytearray(struct.pack("<II", 20000630, 2))
+
+    def attr(name, typ, val):
+        out.extend(name.encode() + b"\0" + typ.encode() + b"\0" + struct.pack("<i", len(val)) + val)
+    ch = b"".join(c.encode() + b"\0" + struct.pack("<iBBBBii", ptype, 0, 0, 0, 0, 1, 1) for c in "BGR") + b"\0"
+    attr("channels", "chlist", ch)
+    attr("compression", "compression", bytes([comp]))
+    attr("dataWindow", "box2i", struct.pack("<iiii", 0, 0, W - 1, H - 1))
+    attr("displayWindow", "box2i", struct.pack("<iiii", 0, 0, W - 1, H - 1))
+    attr("lineOrder", "lineOrder", b"\0")
+    out.extend(b"\0")
+    table = len(out)
+    out.extend(b"\0" * 8 * H)
+    dt = "<f2" if ptype == 1 else "<f4"
+    for y in range(H):
+        raw = b"".join(rgb[y, :, c].astype(dt).tobytes() for c in (2, 1, 0))
+        data = raw
+        if comp == 2:
+            a = np.frombuffer(raw, np.uint8)
+            t = np.concatenate([a[0::2], a[1::2]]).astype(np.int32)
+            d = t.copy()
+            d[1:] = (t[1:] - t[:-1] + 128) & 0xFF
+            z = zlib.compress(d.astype(np.uint8).tobytes())
+            data = z if len(z) < len(raw) else raw
+        struct.pack_into("<Q", out, table + 8 * y, len(out))
+        out.extend(struct.pack("<ii", y, len(data)) + data)
+    open(path, "wb").write(bytes(out))
+
+
+def test_exr_reader_matches_golden_decoder(mrt_mod):
+    """libmrt's EXR reader (mrt_image_load_exr, the loadReferenceImage
+    replacement, renderer/Renderer.mm:162-253) decodes the reference's own
+    Mitsuba golden (ZIP, half RGB, 800x600) bit for bit like the test
+    decoder tests/exr.py, flipped to row 0 = bottom, A = 1."""
+    import exr
+    path = os.path.join(ROOT, "tests", "golden", "white-box-2.exr")
+    got = mrt_mod.load_exr(path)
+    want = exr.read_rgb(path)[::-1]
+    assert got.shape == (600, 800, 4)
+    assert got[..., :3].tobytes() == np.ascontiguousarray(want).tobytes()
+    assert np.all(got[..., 3] == 1.0)
+
+
+@pytest.mark.parametrize("comp,ptype", [(0, 2), (0, 1), (2, 1), (2, 2)])
+def test_exr_reader_formats(mrt_mod, tmp_path, comp, ptype):
+    """NONE / ZIPS compression, HALF / FLOAT channels, odd sizes."""
+    import exr
+    rng = np.random.default_rng(comp * 7 + ptype)
+    rgb = (rng.standard_normal((13, 37, 3)) * 4).astype(np.float16 if ptype == 1 else np.float32).astype(np.float32)
+    rgb[0, 0] = [0.0, 65504.0 if ptype == 1 else 1e30, -2.5e-7]   # zero, max half / huge float, subnormal-ish
+    rgb = rgb.astype(np.float16).astype(np.float32) if ptype == 1 else rgb
+    p = str(tmp_path / "t.exr")
+    _write_exr(p, rgb, comp, ptype)
+    got = mrt_mod.load_exr(p)
+    assert np.array_equal(got[::-1, :, :3], rgb) and np.array_equal(got[..., :3], exr.read_rgb(p)[::-1])
+    with pytest.raises(mrt_mod.MrtError, match="OpenEXR|open"):
+        mrt_mod.load_exr(str(tmp_path / "missing.exr"))
