@@ -575,10 +575,10 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (const char* v = std::getenv("MRT_BINS")) opt.bins = (uint32_t)std::strtoul(v, nullptr, 0);
   if (const char* v = std::getenv("MRT_EXACT_SAH")) opt.exact_sah_below = (uint32_t)std::strtoul(v, nullptr, 0);
   const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
-  // default width: BVH4 for scenes small enough to be staged whole in LDS
-  // (quadrant-copy nodes, kernels.hip kAllLds), the compressed BVH8 for
-  // scenes traversed from global memory; the device builders emit BVH4
-  opt.width = desc->bvh_width ? desc->bvh_width : (builder != MRT_BVH_HOST_SAH || T <= 256 ? 4 : 8);
+  // default width 4: the compressed BVH8 (bvh_width = 8) halves the node
+  // bytes but measured slower on every global-memory scene (C4 -33 %, C3
+  // -26 %: 1.85x the VALU instructions per launch)
+  opt.width = desc->bvh_width ? desc->bvh_width : 4;
   if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
   if (opt.width != 2 && opt.width != 4 && opt.width != 8) return fail(MRT_ERR_INVALID, "bvh_width must be 2, 4 or 8");
   if (opt.width == 8 && opt.max_leaf_size > 3) opt.max_leaf_size = 3;   // BVH8 leaf slots hold <= 3 triangles

@@ -53,11 +53,12 @@ def test_c2_full_size_matches_oracle(gpu, mrt_mod, c2_oracle, build):
         assert abs(st["active_ray_bounces"] - A) <= A // 1000
 
 
-@pytest.fixture(scope="module")
-def big_scene(gpu, mrt_mod, oracle_mod):
+@pytest.fixture(scope="module", params=[4, 8], ids=["bvh4", "bvh8"])
+def big_scene(gpu, mrt_mod, oracle_mod, request):
     """C4/C5's scene: cornellbox + the seeded 1M-triangle displaced sphere
-    (host SAH BVH4), and the oracle over the same flattened buffers."""
-    sc = mrt_mod.Scene("cornellbox", procedural_triangles=PROC)
+    (host SAH BVH4, the default, and the compressed BVH8), and the oracle
+    over the same flattened buffers."""
+    sc = mrt_mod.Scene("cornellbox", procedural_triangles=PROC, bvh_width=request.param)
     e = sc.export()
     osc = oracle_mod.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
     assert sc.info["triangles"] == PROC + 36

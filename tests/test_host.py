@@ -88,7 +88,7 @@ def test_bvh8_compressed_structure(mrt_mod):
 
 def test_bvh_width_default_and_invalid(mrt_mod):
     assert mrt_mod.Scene("cornellbox", device=-1).info["bvh_width"] == 4
-    assert mrt_mod.Scene("CornellBox-Water-plastic", device=-1).info["bvh_width"] == 8   # global-memory scenes
+    assert mrt_mod.Scene("CornellBox-Water-plastic", device=-1).info["bvh_width"] == 4
     with pytest.raises(mrt_mod.MrtError, match="bvh_width"):
         mrt_mod.Scene("cornellbox", device=-1, bvh_width=3)
 
@@ -100,7 +100,7 @@ def test_bvh_procedural_mesh(mrt_mod):
     s2 = mrt_mod.Scene("cornellbox", device=-1, procedural_triangles=1 << 16, procedural_seed=3, bvh_width=2)
     s2.check_bvh()
     assert s2.info["bvh_max_stack"] == s2.info["bvh_depth"] < s.info["bvh_max_stack"] <= 48
-    s8 = mrt_mod.Scene("cornellbox", device=-1, procedural_triangles=1 << 16, procedural_seed=3)
+    s8 = mrt_mod.Scene("cornellbox", device=-1, procedural_triangles=1 << 16, procedural_seed=3, bvh_width=8)
     s8.check_bvh()
     assert s8.info["bvh_width"] == 8 and s8.info["bvh_max_stack"] < s2.info["bvh_depth"]
     e = s.export()
