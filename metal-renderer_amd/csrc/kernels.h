@@ -48,6 +48,8 @@ static_assert(kGrabRanges <= 31, "kGrabRanges");
 #endif
 constexpr uint32_t kGrabStride = MRT_GRAB_STRIDE;    // uint32 words between counters
 constexpr uint32_t kSegSlack = 1024;
+constexpr uint32_t kRefillSlack = 2048;   // segment slack of the lane-refill kernel (kernels.hip)
+constexpr uint32_t kMaxSegSlack = kRefillSlack;
 
 struct BounceArgs {
   uint32_t width, height;

@@ -1401,6 +1401,383 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Lane-refill bounce kernel (global-memory scenes: kTopLds / kGlobal).
+//
+// In bounce_kernel a wave runs its 64 rays through nearest hit, shading and
+// the shadow query in lockstep, so every traversal phase lasts as long as its
+// slowest lane: on incoherent secondary rays over the 1M-triangle BVH the
+// SIMD efficiency of the traversal loop is ~0.3 (tools/bvh_stats.cpp).  Here
+// each lane carries a resumable traversal (node, parked leaf, stack) and the
+// wave runs traversal rounds until kRefillService lanes have finished their
+// query; the finished lanes are then serviced together — a finished nearest
+// query is shaded (MIS emission, next ray into the output queue, NEE shadow
+// ray that starts its occlusion query right away), a finished shadow query
+// adds its contribution and writes the ray's radiance plane — and idle lanes
+// take new rays from the wave's grab pool (persistent threads with dynamic
+// ray fetch, Aila & Laine 2009).  The arithmetic per ray is the same as in
+// bounce_kernel, so the image is identical (precise build: bitwise).
+// ---------------------------------------------------------------------------
+#ifndef MRT_REFILL_SERVICE
+#define MRT_REFILL_SERVICE 24
+#endif
+// 4 waves/SIMD: the resumable lane state keeps ~118 VGPRs live through the
+// shading of the finished lanes; at 5 waves (96 VGPRs) 85 of them spill and
+// C4 ran 10 % slower (tools/lib_sweep.sh, r2)
+#ifndef MRT_REFILL_WAVES
+#define MRT_REFILL_WAVES 4
+#endif
+
+struct Trav {
+  int32_t node, leaf;
+  int sp;
+};
+// words of lane state the refill kernel parks in LDS around a service phase
+// ([word][lane] after the traversal stack): ro, rd, h.t, h.u, h.v, h.prim,
+// tr.node, tr.leaf, tr.sp, aux0, aux1, flags
+constexpr uint32_t kLaneStateWords = 16;
+
+__device__ __forceinline__ void trav_begin(const DeviceScene& sc, Trav& tr) {
+  tr.node = sc.root;
+  tr.leaf = 0;
+  tr.sp = 0;
+  if (tr.node < 0) { tr.leaf = tr.node; tr.node = kDone; }
+}
+__device__ __forceinline__ bool trav_done(const Trav& tr) { return tr.node == kDone && tr.leaf == 0; }
+
+// One round of the while-while walk of traverse(): interior nodes (parking
+// one leaf) until every lane still descending holds a leaf, then the parked
+// leaves.  any = occlusion query: stops at the first triangle k != target
+// with (t_k, k) < (h.t, target) and sets `occluded`.
+template <int STACK, int MODE, int WIDTH>
+__device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, const RayBox& rb,
+                                           Hit& h, bool any, uint32_t target, bool& occluded, Trav& tr) {
+  while (tr.node != kDone && tr.node >= 0) {
+    tr.node = interior_step<STACK, MODE, WIDTH, false>(sc, cx, tr.node, o, rb, 0.0f, h.t, tr.sp);
+    if (tr.node < 0 && tr.leaf == 0) {
+      tr.leaf = tr.node;
+      tr.node = stack_pop<STACK>(cx, tr.sp);
+    }
+    if (!__any(tr.leaf == 0)) break;
+  }
+  while (tr.leaf < 0) {
+    const uint32_t lr = ~(uint32_t)tr.leaf;
+    const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
+    bool stop = false;
+    for (uint32_t k = 0; k < cnt; ++k) {
+      float4 t0, t1, t2;
+      fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
+      const uint32_t prim = fbits(t0.w);
+      float t, u, v;
+      const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), 0.0f, h.t, t, u, v);
+      if (any) {
+        if (hit & (prim != target) & ((t < h.t) | (prim < target))) { stop = true; break; }
+      } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
+        h.found = true;
+        h.t = t;
+        h.u = u;
+        h.v = v;
+        h.prim = prim;
+      }
+    }
+    if (stop) {   // occluded: the query is over
+      occluded = true;
+      tr.node = kDone;
+      tr.leaf = 0;
+      break;
+    }
+    tr.leaf = 0;
+    if (tr.node < 0) {
+      tr.leaf = tr.node;
+      tr.node = stack_pop<STACK>(cx, tr.sp);
+    }
+  }
+}
+
+template <int STACK, int MODE, int WIDTH>
+__global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel(DeviceScene sc, BounceArgs a) {
+  __shared__ uint32_t s_wave[kBlock / 64];
+  __shared__ uint32_t s_cursor[2], s_res, s_closed;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t G = gridDim.x;
+  const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
+  const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1, a.stack_spill);
+  uint32_t* seg = lds_u32() + cx.scratch_base;
+  if (tid == 0) s_cursor[0] = s_cursor[1] = s_res = s_closed = 0;
+  uint32_t N, in_chunk = 0;
+  if (a.bounce == 0) {
+    N = a.num_slots * a.batch;
+    __syncthreads();
+  } else {
+    for (uint32_t i = tid; i < nseg; i += kBlock) seg[i] = a.in_seg_count[i];
+    __syncthreads();
+    N = block_exclusive_scan(seg, nseg, s_wave);
+    if (tid == 0) seg[nseg] = N;
+    __syncthreads();
+    in_chunk = *a.in_chunk;
+  }
+  const uint32_t chunk = ((N + G - 1) / G + kBlock - 1) / kBlock * kBlock;
+  // output reservation (see bounce_kernel): a wave reserves kGrab slots per
+  // grab; a ray holds one slot from the grab until it is shaded, when a
+  // survivor fills it and a finished path releases it (as do the grab's
+  // indices past its range and bounce-0 slots outside the image).  A wave
+  // thus holds at most kGrab (pool) + 64 (in flight) unfilled slots, 768 per
+  // block, below the slack kRefillSlack: a block that cannot reserve has
+  // written more than `chunk` survivors, so not every block can stop while
+  // input remains
+  const uint32_t cap = chunk + kRefillSlack;
+  const uint32_t out_base = blockIdx.x * cap;
+  const uint32_t rlen = ((N + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
+  uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
+  const uint32_t lane = tid & 63u;
+  const bool last = (a.bounce + 1 == a.max_path_length);
+  const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t back = (a.bounce % 3u) == 0 ? 0u : ((a.bounce % 3u) == 1 ? 2u : 1u);
+  // this lane's parked-state words: after the traversal stack (kLaneStateWords x [word][lane])
+  const uint32_t st_base = cx.stack_base + (uint32_t)(STACK < 0 ? -STACK : STACK) * kBlock;
+
+  // wave-uniform pool of input indices [pool_next, pool_end) of the current grab
+  uint32_t pool_next = 0, pool_end = 0;
+  bool exhausted = false;
+  // lane state (registers are tight: everything a traversing lane keeps is
+  // live while other lanes shade, so the two queries share registers)
+  uint32_t phase = 0;                 // 0 idle, 1 nearest query, 2 shadow query
+  V3 ro = mk(0.0f, 0.0f, 0.0f), rd = mk(0.0f, 0.0f, 1.0f);
+  Trav tr{kDone, 0, 0};
+  Hit h;                              // nearest: the hit; shadow: h.t = t_target, (h.u, h.v, h.prim) = the
+  h.t = 0.0f; h.u = h.v = 0.0f;       //   light contribution L (x, y, bits of z)
+  h.prim = 0u; h.found = false;
+  bool occluded = false;
+  uint32_t aux0 = 0, aux1 = 0;        // nearest: (global slot | prevDiffuse << 31, input queue slot);
+                                      // shadow: (light triangle, output queue slot)
+
+  for (;;) {
+    // ---- refill idle lanes from the pool (grab when it runs dry)
+    for (;;) {
+      const uint64_t idle = __ballot(phase == 0);
+      if (!idle || exhausted) break;
+      if (pool_next >= pool_end) {
+        uint32_t got = 0xFFFFFFFFu;
+        if (lane == 0) {
+          if (atomicAdd(&s_res, kGrab) + kGrab <= cap) {
+            while (ranges_left) {
+              const uint32_t r0 = cur_range * rlen;
+              if (r0 < N && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
+                const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
+                if (i < rlen && r0 + i < N) { got = r0 + i; break; }
+                atomicOr(&s_closed, 1u << cur_range);
+              }
+              cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
+              --ranges_left;
+            }
+            if (got == 0xFFFFFFFFu) atomicSub(&s_res, kGrab);
+          } else {
+            got = 0xFFFFFFFEu;   // the block's output segment is full
+          }
+        }
+        got = __builtin_amdgcn_readfirstlane(got);
+        cur_range = __builtin_amdgcn_readfirstlane(cur_range);
+        ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
+        if (got >= 0xFFFFFFFEu) { exhausted = true; break; }
+        pool_next = got;
+        pool_end = min(N, min(got + kGrab, cur_range * rlen + rlen));
+        if (lane == 0 && pool_end - pool_next < kGrab) atomicSub(&s_res, kGrab - (pool_end - pool_next));
+      }
+      const uint32_t rank = (uint32_t)__popcll(idle & lanes_below);
+      const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool_next);
+      bool ok = true;
+      if (phase == 0 && rank < take) {
+        const uint32_t idx = pool_next + rank;
+        if (a.bounce == 0) {
+          const uint32_t fj = a.batch == 1u ? 0u : idx / a.num_slots;
+          uint32_t x, y;
+          slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+          ok = (x < a.width) && (y < a.height);
+          if (ok) {
+            aux0 = idx;
+            const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
+            camera_ray(x, y, a.width, a.height, ns, ro, rd);
+          }
+        } else {
+          uint32_t lo = 0, hi = nseg;
+          while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
+          const uint32_t g_in = nseg >> 1;
+          aux1 = lo < g_in ? lo * in_chunk + (idx - seg[lo])
+                           : (lo - g_in) * in_chunk + in_chunk - (seg[lo + 1] - seg[lo]) + (idx - seg[lo]);
+          const float4 q0 = a.in_q.plane[0][aux1], q1 = a.in_q.plane[1][aux1];
+          ro = mk(q0);
+          aux0 = fbits(q0.w);
+          rd = mk(q1);
+        }
+        if (ok) {
+          phase = 1;
+          trav_begin(sc, tr);
+          h.t = __builtin_inff();
+          h.u = h.v = 0.0f;
+          h.prim = 0xFFFFFFFFu;
+          h.found = false;
+        }
+      }
+      const uint64_t bad = __ballot(!ok);   // bounce-0 slots outside the image release their output slot
+      if (lane == 0 && bad) atomicSub(&s_res, (uint32_t)__popcll(bad));
+      pool_next += take;
+    }
+    if (!__any(phase != 0)) break;   // every lane idle and no input left
+
+    // ---- traversal rounds until enough lanes have finished their query
+    bool fin = phase != 0 && trav_done(tr);
+    for (;;) {
+      const uint64_t going = __ballot(phase != 0 && !fin);
+      if (!going) break;
+      if ((uint32_t)__popcll(__ballot(fin)) >= (exhausted ? 1u : (uint32_t)MRT_REFILL_SERVICE)) break;
+      if (phase != 0 && !fin) {
+        const RayBox rb = make_raybox(ro, rd);   // recomputed per round: not live across shading
+        trav_round<STACK, MODE, WIDTH>(sc, cx, ro, rd, rb, h, phase == 2, aux0, occluded, tr);
+        fin = trav_done(tr);
+      }
+    }
+
+    if (!__any(fin)) continue;
+
+    // ---- service.  Every lane's state is parked in LDS first, so while the
+    //      finished lanes shade, the traversing lanes' registers are free
+    //      (the live set of the shading code alone fits the register budget)
+    uint32_t* const ls = lds_u32() + st_base;
+    ls[0 * kBlock] = fbits(ro.x); ls[1 * kBlock] = fbits(ro.y); ls[2 * kBlock] = fbits(ro.z);
+    ls[3 * kBlock] = fbits(rd.x); ls[4 * kBlock] = fbits(rd.y); ls[5 * kBlock] = fbits(rd.z);
+    ls[6 * kBlock] = fbits(h.t); ls[7 * kBlock] = fbits(h.u); ls[8 * kBlock] = fbits(h.v); ls[9 * kBlock] = h.prim;
+    ls[10 * kBlock] = (uint32_t)tr.node; ls[11 * kBlock] = (uint32_t)tr.leaf; ls[12 * kBlock] = (uint32_t)tr.sp;
+    ls[13 * kBlock] = aux0; ls[14 * kBlock] = aux1;
+    ls[15 * kBlock] = phase | (h.found ? 4u : 0u) | (occluded ? 8u : 0u) | (fin ? 16u : 0u);
+    {
+      const uint32_t flags = ls[15 * kBlock];
+      const uint32_t ph = flags & 3u;
+      const bool done = (flags & 16u) != 0;
+      // finished shadow queries (MPS nearest-hit semantics + lightSamplingHandler,
+      // Shaders.metal:214-231): the ray's radiance plane was written without
+      // the light; add it when the target is visible
+      if (done && ph == 2) {
+        const uint32_t os = ls[14 * kBlock];
+        if (!(flags & 8u)) {
+          const float4 q3 = a.out_q.plane[3][os];
+          a.out_q.plane[3][os] = make_float4(q3.x + bitsf(ls[7 * kBlock]), q3.y + bitsf(ls[8 * kBlock]),
+                                             q3.z + bitsf(ls[9 * kBlock]), q3.w);
+        }
+        ls[15 * kBlock] = 0u;
+      }
+      // finished nearest queries (intersectionHandler, Shaders.metal:105-212)
+      const bool shade_now = done && ph == 1;
+      PathState s;
+      ShadowRay sh;
+      sh.valid = false;
+      bool hit_ok = false;
+      uint32_t gslot = 0, tagv = 0;
+      Hit hh;
+      if (shade_now) {
+        s.o = mk(bitsf(ls[0 * kBlock]), bitsf(ls[1 * kBlock]), bitsf(ls[2 * kBlock]));
+        s.d = mk(bitsf(ls[3 * kBlock]), bitsf(ls[4 * kBlock]), bitsf(ls[5 * kBlock]));
+        hh.t = bitsf(ls[6 * kBlock]); hh.u = bitsf(ls[7 * kBlock]); hh.v = bitsf(ls[8 * kBlock]);
+        hh.prim = ls[9 * kBlock]; hh.found = (flags & 4u) != 0;
+        tagv = ls[13 * kBlock];
+        s.prevDiffuse = (tagv >> 31) ? 1.0f : 0.0f;
+        gslot = tagv & 0x7FFFFFFFu;
+        if (a.bounce == 0) {
+          s.T = mk(1.0f, 1.0f, 1.0f);
+          s.R = mk(0.0f, 0.0f, 0.0f);
+          s.pdf = 1.0f;
+          s.prevDiffuse = 0.0f;
+          s.ior = 1.00029f;
+        } else {
+          const uint32_t is = ls[14 * kBlock];
+          const float4 q2 = a.in_q.plane[2][is], q3 = a.in_q.plane[3][is];
+          s.T = mk(q2);
+          s.pdf = q2.w;
+          s.R = mk(q3);
+          s.ior = q3.w;
+        }
+        hit_ok = hh.found && !(hh.t < kDistanceEpsilon);
+        if (hit_ok) {
+          const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;
+          uint32_t x, y;
+          slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+          const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, a.bounce, a.frame_index + fj)];
+          shade_hit<MODE>(sc, cx, hh, s, ns, a.bounce, a.max_path_length, !last, sh);
+        }
+        if (!hit_ok || last) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
+      }
+      // survivors -> this block's segment of the next queue (material classes)
+      const bool alive = shade_now && hit_ok && !last;
+      const bool cls1 = (s.prevDiffuse == 0.0f) && !(a.debug & 16u);
+      const uint64_t mask0 = __ballot(alive && !cls1), mask1 = __ballot(alive && cls1);
+      uint32_t oslot = 0;
+      if (mask0 | mask1) {
+        uint32_t w0 = 0, w1 = 0;
+        if (lane == 0) {
+          if (mask0) w0 = atomicAdd(&s_cursor[0], (uint32_t)__popcll(mask0));
+          if (mask1) w1 = atomicAdd(&s_cursor[1], (uint32_t)__popcll(mask1));
+        }
+        w0 = __shfl(w0, 0);
+        w1 = __shfl(w1, 0);
+        if (alive) {
+          oslot = cls1 ? out_base + cap - 1u - (w1 + (uint32_t)__popcll(mask1 & lanes_below))
+                       : out_base + w0 + (uint32_t)__popcll(mask0 & lanes_below);
+          a.out_q.plane[0][oslot] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
+          a.out_q.plane[1][oslot] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
+          a.out_q.plane[2][oslot] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
+          a.out_q.plane[3][oslot] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
+        }
+      }
+      const uint64_t ended = __ballot(shade_now && !alive);   // finished paths release their output slot
+      if (lane == 0 && ended) atomicSub(&s_res, (uint32_t)__popcll(ended));
+      if (shade_now) {
+        uint32_t nflags = 0u;
+        if (alive && sh.valid) {
+          // the shadow ray: MPS nearest hit == target test + occlusion query
+          // (shadow_reaches_target); the query runs in the next rounds
+          const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
+          const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
+          float tT, u, v;
+          if (tri_test(sh.o, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
+              !(tT < kDistanceEpsilon)) {
+            Trav t0;
+            trav_begin(sc, t0);
+            ls[0 * kBlock] = fbits(sh.o.x); ls[1 * kBlock] = fbits(sh.o.y); ls[2 * kBlock] = fbits(sh.o.z);
+            ls[3 * kBlock] = fbits(sh.d.x); ls[4 * kBlock] = fbits(sh.d.y); ls[5 * kBlock] = fbits(sh.d.z);
+            ls[6 * kBlock] = fbits(tT);
+            ls[7 * kBlock] = fbits(sh.L.x); ls[8 * kBlock] = fbits(sh.L.y); ls[9 * kBlock] = fbits(sh.L.z);
+            ls[10 * kBlock] = (uint32_t)t0.node; ls[11 * kBlock] = (uint32_t)t0.leaf; ls[12 * kBlock] = 0u;
+            ls[13 * kBlock] = sh.target;
+            ls[14 * kBlock] = oslot;
+            nflags = 2u;
+          }
+        }
+        ls[15 * kBlock] = nflags;
+      }
+    }
+    // ---- every lane resumes from its parked (or new) state
+    ro = mk(bitsf(ls[0 * kBlock]), bitsf(ls[1 * kBlock]), bitsf(ls[2 * kBlock]));
+    rd = mk(bitsf(ls[3 * kBlock]), bitsf(ls[4 * kBlock]), bitsf(ls[5 * kBlock]));
+    h.t = bitsf(ls[6 * kBlock]); h.u = bitsf(ls[7 * kBlock]); h.v = bitsf(ls[8 * kBlock]); h.prim = ls[9 * kBlock];
+    tr.node = (int32_t)ls[10 * kBlock]; tr.leaf = (int32_t)ls[11 * kBlock]; tr.sp = (int)ls[12 * kBlock];
+    aux0 = ls[13 * kBlock]; aux1 = ls[14 * kBlock];
+    {
+      const uint32_t flags = ls[15 * kBlock];
+      phase = flags & 3u;
+      h.found = (flags & 4u) != 0;
+      occluded = (flags & 8u) != 0;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    a.out_seg_count[blockIdx.x] = s_cursor[0];
+    a.out_seg_count[G + blockIdx.x] = s_cursor[1];
+    const uint32_t total = s_cursor[0] + s_cursor[1];
+    if (total) atomicAdd(a.out_total, total);
+    if (blockIdx.x == 0) *a.out_chunk = cap;
+  }
+}
+
 // accumulateImage (renderer/Shaders.metal:233-249) for a batch of frames over
 // the owned tiles: image = f == 0 ? c : mix(c, image, f/(f+1)).  Frames are
 // accumulated strictly in order (the running mean is order-dependent): one
@@ -1546,12 +1923,13 @@ int choose_mode(const DeviceScene& sc) {
   return sc.lds_nodes > 0 ? kTopLds : kGlobal;
 }
 
-size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
+size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid, bool refill) {
   const size_t scene = (size_t)lds_scene_float4s(mode, node_float4s(sc.width), sc.num_nodes, sc.lds_nodes,
                                                  sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16;
   const size_t scratch = ((size_t)2 * grid + 1 + 3) / 4 * 16;   // 2 segments per block + sentinel
   const size_t entry_words = sc.width == 8 ? 2 : 1;              // BVH8: two-word group entries
-  return scene + scratch + (size_t)stack * entry_words * kBlock * 4;   // stack = LDS entries (|STACK|)
+  const size_t lane_state = refill ? (size_t)kLaneStateWords * kBlock * 4 : 0;   // lane-refill kernel
+  return scene + scratch + (size_t)stack * entry_words * kBlock * 4 + lane_state;   // stack = LDS entries (|STACK|)
 }
 
 // kTopLds: stage only as many top BVH nodes as keep the block's LDS within
@@ -1563,16 +1941,34 @@ size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_
 #ifndef MRT_LDS_BLOCKS
 #define MRT_LDS_BLOCKS MRT_BOUNCE_WAVES
 #endif
-constexpr size_t kLdsPerBlockTarget = 160 * 1024 / MRT_LDS_BLOCKS - 2048;
+#ifndef MRT_REFILL_LDS_BLOCKS
+#define MRT_REFILL_LDS_BLOCKS 4   // the lane-refill kernel's resident blocks per CU (MRT_REFILL_WAVES)
+#endif
+bool refill_enabled();
 DeviceScene fit_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
   if (mode != kTopLds) return sc;
   DeviceScene f = sc;
-  const size_t fixed = bounce_lds_bytes(sc, kGlobal, stack, grid) + 64;   // scratch + stack + static
+  const bool refill = sc.width != 8 && refill_enabled();
+  const size_t blocks = refill ? MRT_REFILL_LDS_BLOCKS : MRT_LDS_BLOCKS;
+  const size_t kLdsPerBlockTarget = 160 * 1024 / blocks - 2048;
+  const size_t fixed = bounce_lds_bytes(sc, kGlobal, stack, grid, refill) + 64;   // scratch + stack + lane state + static
   const size_t node_bytes = (size_t)node_float4s(sc.width) * 16;
   const size_t fit = fixed < kLdsPerBlockTarget ? (kLdsPerBlockTarget - fixed) / node_bytes : 0;
   f.lds_nodes = (uint32_t)std::min<size_t>(sc.lds_nodes, fit);
   return f;
 }
+
+// the lane-refill kernel serves the global-memory modes (MRT_REFILL=0 keeps
+// bounce_kernel there, for A/B measurements)
+bool refill_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("MRT_REFILL");
+    return !v || std::atoi(v) != 0;
+  }();
+  return on;
+}
+template <int MODE, int WIDTH>
+bool use_refill() { return MODE != kAllLds && WIDTH != 8 && refill_enabled(); }
 
 template <int STACK, int MODE, int WIDTH>
 hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* grid) {
@@ -1590,9 +1986,11 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* gri
   int n = 1;
   for (int want = 8; want >= 1; --want) {
     const uint32_t g = cus * (uint32_t)want;
-    const size_t lds = bounce_lds_bytes(fit_lds_nodes(sc, MODE, stack, g), MODE, stack, g);
+    const size_t lds = bounce_lds_bytes(fit_lds_nodes(sc, MODE, stack, g), MODE, stack, g, use_refill<MODE, WIDTH>());
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bounce_kernel<STACK, MODE, WIDTH>, kBlock, lds) != hipSuccess)
+    const void* fn = use_refill<MODE, WIDTH>() ? (const void*)bounce_refill_kernel<STACK, MODE, WIDTH>
+                                               : (const void*)bounce_kernel<STACK, MODE, WIDTH>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBlock, lds) != hipSuccess)
       occ = 0;
     if (occ >= want) { n = want; break; }
   }
@@ -1606,8 +2004,9 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* gri
 template <int STACK, int MODE, int WIDTH>
 hipError_t launch_bounce_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
   const DeviceScene f = fit_lds_nodes(sc, MODE, STACK < 0 ? -STACK : STACK, grid);
-  const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, grid);
-  bounce_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
+  const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, grid, use_refill<MODE, WIDTH>());
+  if (use_refill<MODE, WIDTH>()) bounce_refill_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
+  else bounce_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
   return hipGetLastError();
 }
 

@@ -282,7 +282,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
   if (owned_slots >= ((size_t)1 << 31)) return fail(MRT_ERR_INVALID, "frame too large");
   // queue capacity: every owned slot of the batch + per-block rounding and
   // slack of the segments (kernels.h)
-  const size_t slots = owned_slots * r->batch + (size_t)r->grid * (256 + mrt::kSegSlack);
+  const size_t slots = owned_slots * r->batch + (size_t)r->grid * (256 + mrt::kMaxSegSlack);
   for (FrameSlot& fs : r->slots) {
     HIP_TRY(fs.segments.alloc(((size_t)4 * r->grid + 2) * 4));   // 2 queues x 2 classes x grid + 2 chunk words
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));

@@ -22,7 +22,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(path, kernel="bounce_kernel"):
+def counters(path, kernel="bounce_"):
     agg, n = collections.defaultdict(float), collections.Counter()
     meta = {}
     for r in csv.DictReader(open(path)):
@@ -45,7 +45,7 @@ def main(tag="r1", cfg="c2"):
     write, _ = counters(os.path.join(src, "write", "run_counter_collection.csv"))
     sq, _ = counters(os.path.join(src, "sq", "run_counter_collection.csv"))
     clk, _ = counters(os.path.join(src, "clk", "run_counter_collection.csv"))
-    bounce = next(r for r in rows if "bounce_kernel" in r["Name"])
+    bounce = next(r for r in rows if "bounce_" in r["Name"])
     avg_ns = float(bounce["AverageNs"])
     hbm = (2.0 * fetch["FETCH_SIZE"] + write["WRITE_SIZE"]) * 1024.0
     lines = [f"# rocprofv3 summary — {tag} / {cfg}", "",
