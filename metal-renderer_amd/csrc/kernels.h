@@ -84,6 +84,7 @@ struct BounceArgs {
                                // owned pixel when its path ends (accumulated by launch_accumulate_frame)
   uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
                                // [max_stack - stack_entries][grid * 256] uint32 (null if none)
+  uint32_t* bounce_counts;     // path kernel: [max_path_length] rays alive at the start of bounce b + 1
 };
 
 // running-mean accumulation of one frame over the owned tiles
@@ -117,6 +118,12 @@ struct AccumArgs {
      stack_entries = LDS stack capacity 8/16/24/32, deeper entries go to a.stack_spill */                 \
   hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
                            uint32_t grid, hipStream_t s);                                                 \
+  /* path megakernel: every bounce of a batch of frames in one launch (a.bounce unused, no ray queues) */ \
+  hipError_t launch_paths(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,            \
+                          uint32_t grid, hipStream_t s);                                                  \
+  hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                   \
+  /* the scene's LDS staging mode is not "whole scene in LDS": the path kernel is the faster one */      \
+  bool path_preferred(const DeviceScene& sc);                                                             \
   /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \
   hipError_t launch_accumulate_frame(const AccumArgs& a, hipStream_t s);                                  \
   /* blitFragment (Shaders.metal:33-70): tone map / sRGB / golden comparison of the RGBA32F image */     \

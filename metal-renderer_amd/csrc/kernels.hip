@@ -1778,6 +1778,209 @@ __global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Path megakernel: all MAX_PATH_LENGTH bounces of a batch of frames in ONE
+// launch.  Each lane carries a whole path — camera ray, then per bounce the
+// nearest-hit query, intersectionHandler, the NEE shadow query and
+// lightSamplingHandler, in the reference's order (renderer/Renderer.mm:
+// 500-585) — as a sequence of resumable traversal queries (trav_round); when
+// kRefillService lanes have finished their query the wave services them
+// together (shading or the shadow resolve, then the next query of the same
+// path), and a lane whose path ended takes the next pixel sample from the
+// wave's grab pool.  Compared with the wavefront of per-bounce launches there
+// are no ray queues in HBM (the path state lives in LDS, 64 B per lane), no
+// compaction and segment scans, and one launch (one ramp and drain) per
+// batch instead of one per bounce.  The arithmetic of every path is the
+// same, so the image is identical (precise build: bitwise).
+// LDS path state per lane ([word][lane] after the stack): T (0-2), R (3-5),
+// material pdf (6), ior (7), next-ray origin (8-10) and direction (11-13),
+// pixel slot tag (14), flags (15: prevDiffuse).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPathStateWords = 16;
+#ifndef MRT_PATH_WAVES
+#define MRT_PATH_WAVES 4
+#endif
+#ifndef MRT_PATH_SERVICE
+#define MRT_PATH_SERVICE 24
+#endif
+
+template <int STACK, int MODE, int WIDTH>
+__global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScene sc, BounceArgs a) {
+  __shared__ uint32_t s_closed;
+  __shared__ uint32_t s_count[64];   // rays alive at the start of bounce b + 1 (stats)
+  const uint32_t tid = threadIdx.x;
+  const LdsCtx cx = stage_lds<MODE>(sc, 1, a.stack_spill);
+  if (tid == 0) s_closed = 0;
+  if (tid < 64) s_count[tid] = 0;
+  __syncthreads();
+  const uint32_t N = a.num_slots * a.batch;
+  const uint32_t L = a.max_path_length;
+  const uint32_t rlen = ((N + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
+  uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
+  const uint32_t lane = tid & 63u;
+  uint32_t* const ps = lds_u32() + cx.stack_base + (uint32_t)(STACK < 0 ? -STACK : STACK) * kBlock;
+
+  uint32_t pool_next = 0, pool_end = 0;   // wave-uniform pool of pixel-sample indices
+  bool exhausted = false;
+  uint32_t phase = 0;                     // 0 idle, 1 nearest query, 2 shadow query
+  uint32_t bounce = 0;
+  V3 ro = mk(0.0f, 0.0f, 0.0f), rd = mk(0.0f, 0.0f, 1.0f);
+  Trav tr{kDone, 0, 0};
+  Hit h;                                  // nearest: the hit; shadow: h.t = t_target, (h.u, h.v, bits h.prim) = L
+  h.t = 0.0f; h.u = h.v = 0.0f; h.prim = 0u; h.found = false;
+  bool occluded = false;
+  uint32_t target = 0;
+
+  for (;;) {
+    // ---- refill idle lanes with new camera rays (rayGenerator, Shaders.metal:75-103)
+    for (;;) {
+      const uint64_t idle = __ballot(phase == 0);
+      if (!idle || exhausted) break;
+      if (pool_next >= pool_end) {
+        uint32_t got = 0xFFFFFFFFu;
+        if (lane == 0) {
+          while (ranges_left) {
+            const uint32_t r0 = cur_range * rlen;
+            if (r0 < N && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
+              const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
+              if (i < rlen && r0 + i < N) { got = r0 + i; break; }
+              atomicOr(&s_closed, 1u << cur_range);
+            }
+            cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
+            --ranges_left;
+          }
+        }
+        got = __builtin_amdgcn_readfirstlane(got);
+        cur_range = __builtin_amdgcn_readfirstlane(cur_range);
+        ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
+        if (got == 0xFFFFFFFFu) { exhausted = true; break; }
+        pool_next = got;
+        pool_end = min(N, min(got + kGrab, cur_range * rlen + rlen));
+      }
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+      const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool_next);
+      if (phase == 0 && rank < take) {
+        const uint32_t idx = pool_next + rank;
+        const uint32_t fj = a.batch == 1u ? 0u : idx / a.num_slots;
+        uint32_t x, y;
+        slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+        if ((x < a.width) && (y < a.height)) {
+          const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
+          camera_ray(x, y, a.width, a.height, ns, ro, rd);
+          ps[0 * kBlock] = fbits(1.0f); ps[1 * kBlock] = fbits(1.0f); ps[2 * kBlock] = fbits(1.0f);
+          ps[3 * kBlock] = 0u; ps[4 * kBlock] = 0u; ps[5 * kBlock] = 0u;
+          ps[6 * kBlock] = fbits(1.0f); ps[7 * kBlock] = fbits(1.00029f);
+          ps[14 * kBlock] = idx;
+          ps[15 * kBlock] = 0u;
+          phase = 1;
+          bounce = 0;
+          trav_begin(sc, tr);
+          h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
+        }
+      }
+      pool_next += take;
+    }
+    if (!__any(phase != 0)) break;   // every lane idle and no samples left
+
+    // ---- traversal rounds until enough lanes have finished their query
+    bool fin = phase != 0 && trav_done(tr);
+    for (;;) {
+      const uint64_t going = __ballot(phase != 0 && !fin);
+      if (!going) break;
+      if ((uint32_t)__popcll(__ballot(fin)) >= (exhausted ? 1u : (uint32_t)MRT_PATH_SERVICE)) break;
+      if (phase != 0 && !fin) {
+        const RayBox rb = make_raybox(ro, rd);
+        trav_round<STACK, MODE, WIDTH>(sc, cx, ro, rd, rb, h, phase == 2, target, occluded, tr);
+        fin = trav_done(tr);
+      }
+    }
+    if (!__any(fin)) continue;
+
+    // ---- service: finished shadow queries (MPS nearest hit + lightSamplingHandler,
+    //      Shaders.metal:214-231), then the path's next bounce
+    bool next_query = false;
+    if (fin && phase == 2) {
+      if (!occluded) {
+        ps[3 * kBlock] = fbits(bitsf(ps[3 * kBlock]) + h.u);
+        ps[4 * kBlock] = fbits(bitsf(ps[4 * kBlock]) + h.v);
+        ps[5 * kBlock] = fbits(bitsf(ps[5 * kBlock]) + bitsf(h.prim));
+      }
+      next_query = true;
+    }
+    // ---- service: finished nearest queries (intersectionHandler, Shaders.metal:105-212)
+    if (fin && phase == 1) {
+      PathState s;
+      s.o = ro;
+      s.d = rd;
+      s.T = mk(bitsf(ps[0 * kBlock]), bitsf(ps[1 * kBlock]), bitsf(ps[2 * kBlock]));
+      s.R = mk(bitsf(ps[3 * kBlock]), bitsf(ps[4 * kBlock]), bitsf(ps[5 * kBlock]));
+      s.pdf = bitsf(ps[6 * kBlock]);
+      s.ior = bitsf(ps[7 * kBlock]);
+      s.prevDiffuse = (ps[15 * kBlock] & 1u) ? 1.0f : 0.0f;
+      const uint32_t gslot = ps[14 * kBlock];
+      const bool last = bounce + 1 == L;
+      const bool hit_ok = h.found && !(h.t < kDistanceEpsilon);   // :122-126
+      ShadowRay sh;
+      sh.valid = false;
+      if (hit_ok) {
+        const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;
+        uint32_t x, y;
+        slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+        const uint32_t back = (bounce % 3u) == 0 ? 0u : ((bounce % 3u) == 1 ? 2u : 1u);
+        const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, bounce, a.frame_index + fj)];
+        shade_hit<MODE>(sc, cx, h, s, ns, bounce, L, !last, sh);
+      }
+      if (!hit_ok || last) {   // the path ends: accumulateImage input (Shaders.metal:233-249)
+        a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
+        phase = 0;
+      } else {
+        ps[0 * kBlock] = fbits(s.T.x); ps[1 * kBlock] = fbits(s.T.y); ps[2 * kBlock] = fbits(s.T.z);
+        ps[3 * kBlock] = fbits(s.R.x); ps[4 * kBlock] = fbits(s.R.y); ps[5 * kBlock] = fbits(s.R.z);
+        ps[6 * kBlock] = fbits(s.pdf); ps[7 * kBlock] = fbits(s.ior);
+        ps[8 * kBlock] = fbits(s.o.x); ps[9 * kBlock] = fbits(s.o.y); ps[10 * kBlock] = fbits(s.o.z);
+        ps[11 * kBlock] = fbits(s.d.x); ps[12 * kBlock] = fbits(s.d.y); ps[13 * kBlock] = fbits(s.d.z);
+        ps[15 * kBlock] = s.prevDiffuse != 0.0f ? 1u : 0u;
+        // the shadow ray: MPS nearest hit == target test + occlusion query
+        bool shadow = false;
+        if (sh.valid) {
+          const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
+          const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
+          float tT, u, v;
+          if (tri_test(sh.o, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
+              !(tT < kDistanceEpsilon)) {
+            shadow = true;
+            phase = 2;
+            ro = sh.o;
+            rd = sh.d;
+            trav_begin(sc, tr);
+            h.t = tT;
+            h.u = sh.L.x;
+            h.v = sh.L.y;
+            h.prim = fbits(sh.L.z);
+            h.found = false;
+            target = sh.target;
+            occluded = false;
+          }
+        }
+        next_query = !shadow;
+      }
+    }
+    // ---- the path's next bounce: its nearest-hit query
+    if (next_query) {
+      bounce += 1;
+      atomicAdd(&s_count[bounce - 1], 1u);   // stats: rays alive at the start of this bounce
+      ro = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
+      rd = mk(bitsf(ps[11 * kBlock]), bitsf(ps[12 * kBlock]), bitsf(ps[13 * kBlock]));
+      phase = 1;
+      trav_begin(sc, tr);
+      h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
+    }
+  }
+  __syncthreads();
+  if (tid < 64 && tid + 1 < L && s_count[tid]) atomicAdd(a.bounce_counts + tid, s_count[tid]);
+}
+
 // accumulateImage (renderer/Shaders.metal:233-249) for a batch of frames over
 // the owned tiles: image = f == 0 ? c : mix(c, image, f/(f+1)).  Frames are
 // accumulated strictly in order (the running mean is order-dependent): one
@@ -1999,6 +2202,84 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* gri
   // asks for fewer blocks per CU per launch
   *grid = (uint32_t)(prop.multiProcessorCount * (blocks_per_cu ? std::min<uint32_t>(n, blocks_per_cu) : n));
   return hipSuccess;
+}
+
+// path kernel: LDS = scene image + stack + the per-lane path state; the
+// kTopLds node budget fits MRT_PATH_WAVES resident blocks per CU
+size_t path_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack) {
+  const size_t scene = (size_t)lds_scene_float4s(mode, node_float4s(sc.width), sc.num_nodes, sc.lds_nodes,
+                                                 sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16;
+  return scene + 16 + (size_t)stack * kBlock * 4 + (size_t)kPathStateWords * kBlock * 4;
+}
+DeviceScene fit_path_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack) {
+  if (mode != kTopLds) return sc;
+  DeviceScene f = sc;
+  const size_t target = 160 * 1024 / MRT_PATH_WAVES - 2048;
+  const size_t fixed = path_lds_bytes(sc, kGlobal, stack) + 64 + 256;   // + static (s_count, s_closed)
+  const size_t fit = fixed < target ? (target - fixed) / ((size_t)node_float4s(sc.width) * 16) : 0;
+  f.lds_nodes = (uint32_t)std::min<size_t>(sc.lds_nodes, fit);
+  return f;
+}
+
+template <int STACK, int MODE, int WIDTH>
+hipError_t path_grid_t(const DeviceScene& sc, uint32_t* grid) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return e;
+  const int stack = STACK < 0 ? -STACK : STACK;
+  const size_t lds = path_lds_bytes(fit_path_lds_nodes(sc, MODE, stack), MODE, stack);
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, path_kernel<STACK, MODE, WIDTH>, kBlock, lds) != hipSuccess || occ < 1)
+    occ = 1;
+  *grid = (uint32_t)prop.multiProcessorCount * (uint32_t)std::min(occ, 8);
+  return hipSuccess;
+}
+
+template <int STACK, int MODE, int WIDTH>
+hipError_t launch_path_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
+  const int stack = STACK < 0 ? -STACK : STACK;
+  const DeviceScene f = fit_path_lds_nodes(sc, MODE, stack);
+  path_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), path_lds_bytes(f, MODE, stack), s>>>(f, a);
+  return hipGetLastError();
+}
+
+template <int STACK, int WIDTH>
+hipError_t path_dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
+                              hipStream_t s) {
+  switch (choose_mode(sc)) {
+    case kAllLds:
+      return a ? launch_path_t<STACK, kAllLds, WIDTH>(sc, *a, grid, s) : path_grid_t<STACK, kAllLds, WIDTH>(sc, grid_out);
+    case kTopLds:
+      return a ? launch_path_t<STACK, kTopLds, WIDTH>(sc, *a, grid, s) : path_grid_t<STACK, kTopLds, WIDTH>(sc, grid_out);
+    default:
+      return a ? launch_path_t<STACK, kGlobal, WIDTH>(sc, *a, grid, s) : path_grid_t<STACK, kGlobal, WIDTH>(sc, grid_out);
+  }
+}
+
+template <int STACK>
+hipError_t path_dispatch_width(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
+                               hipStream_t s) {
+  return sc.width == 4 ? path_dispatch_mode<STACK, 4>(sc, a, grid, grid_out, s)
+                       : path_dispatch_mode<STACK, 2>(sc, a, grid, grid_out, s);
+}
+
+// stack variants as for the bounce kernel; BVH8 scenes are not served here
+hipError_t path_dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_entries, uint32_t grid,
+                         uint32_t* grid_out, hipStream_t s) {
+  if (sc.width == 8) return hipErrorInvalidValue;
+  if (sc.max_stack > stack_entries) {
+    if (stack_entries <= 8) return path_dispatch_width<-8>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 16) return path_dispatch_width<-16>(sc, a, grid, grid_out, s);
+    return path_dispatch_width<-32>(sc, a, grid, grid_out, s);
+  }
+  if (stack_entries <= 8) return path_dispatch_width<8>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 12) return path_dispatch_width<12>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 16) return path_dispatch_width<16>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 24) return path_dispatch_width<24>(sc, a, grid, grid_out, s);
+  return path_dispatch_width<32>(sc, a, grid, grid_out, s);
 }
 
 template <int STACK, int MODE, int WIDTH>
@@ -2233,6 +2514,17 @@ hipError_t launch_bounce(const DeviceScene& sc, const BounceArgs& a, uint32_t st
                          hipStream_t s) {
   return dispatch(sc, &a, stack_entries, grid, nullptr, s);
 }
+
+hipError_t launch_paths(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,
+                        hipStream_t s) {
+  return path_dispatch(sc, &a, stack_entries, grid, nullptr, s);
+}
+
+hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid) {
+  return path_dispatch(sc, nullptr, stack_entries, 0, grid, nullptr);
+}
+
+bool path_preferred(const DeviceScene& sc) { return sc.width != 8 && choose_mode(sc) != kAllLds; }
 
 }  // namespace MRT_NS
 }  // namespace mrt

@@ -181,6 +181,7 @@ struct mrt_renderer {
   uint32_t batch = 1;           // frames per bounce launch (frame batching)
   mrt_stats stats{};
   uint32_t stack_entries = 32;
+  bool path_mode = true;   // one path-megakernel launch per frame batch (else L bounce launches, MRT_KERNEL=wave)
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
   Exchange x;
   DevBuf reference, display;   // comparison image (mrt_renderer_load_reference) and blit output
@@ -203,7 +204,7 @@ int finalize_draw(mrt_renderer* r, DrawRecord& d) {
   r->stats.last_draw_ms = ms;
   const uint64_t paths = r->owned_pixels * d.frames;
   r->stats.mpaths_per_s = ms > 0.0f ? (double)paths / (ms * 1e-3) / 1e6 : 0.0;
-  r->stats.kernel_launches += (uint64_t)d.launches * L;
+  r->stats.kernel_launches += (uint64_t)d.launches * (r->path_mode ? 1u : L);
   if (r->desc.flags & MRT_FLAG_PROFILE) {
     for (size_t k = 0; k + 1 < d.events; k += 2) {
       float ms_k = 0.0f;
@@ -286,8 +287,8 @@ int alloc_frame_buffers(mrt_renderer* r) {
   for (FrameSlot& fs : r->slots) {
     HIP_TRY(fs.segments.alloc(((size_t)4 * r->grid + 2) * 4));   // 2 queues x 2 classes x grid + 2 chunk words
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
-    for (int q = 0; q < 2; ++q)
-      for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(slots * 16));
+    for (int q = 0; q < 2; ++q)   // the path kernel keeps the path state in LDS: no ray queues
+      for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(r->path_mode ? 0 : slots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
     // BVH8 group entries are two words: the second plane starts max_stack
@@ -310,6 +311,11 @@ int alloc_frame_buffers(mrt_renderer* r) {
 inline hipError_t launch_bounce(const mrt_renderer* r, const mrt::BounceArgs& a, hipStream_t s) {
   if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, s);
   return mrt::fast::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, s);
+}
+
+inline hipError_t launch_paths(const mrt_renderer* r, const mrt::BounceArgs& a, hipStream_t s) {
+  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_paths(r->scene->dev, a, r->stack_entries, r->grid, s);
+  return mrt::fast::launch_paths(r->scene->dev, a, r->stack_entries, r->grid, s);
 }
 
 inline hipError_t launch_accumulate_frame(const mrt_renderer* r, const mrt::AccumArgs& a, hipStream_t s) {
@@ -1097,8 +1103,20 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     }
     HIP_TRY(hipEventCreateWithFlags(&fs.acc_done, hipEventDisableTiming));
   }
-  HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid)
-                                           : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid));
+  // kernel: scenes traversed from global memory run the path megakernel (all
+  // bounces of a frame batch in one launch: C3 +15 %, C4 +1.5 % over the
+  // wavefront), scenes staged whole in LDS the wavefront of per-bounce
+  // launches (C2: the path kernel is 24 % slower); MRT_KERNEL=path|wave
+  // overrides.  The compressed BVH8 is traversed by the wavefront kernels only.
+  r->path_mode = mrt::fast::path_preferred(desc->scene->dev);
+  if (const char* k = std::getenv("MRT_KERNEL"))
+    r->path_mode = desc->scene->dev.width != 8 && std::strcmp(k, "path") == 0;
+  if (r->path_mode)
+    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::path_grid(desc->scene->dev, r->stack_entries, &r->grid)
+                                             : mrt::fast::path_grid(desc->scene->dev, r->stack_entries, &r->grid));
+  else
+    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid)
+                                             : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid));
   if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
   int rc = alloc_frame_buffers(r.get());
   if (rc) return rc;
@@ -1151,9 +1169,10 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
   if (r->grabs.bytes < (size_t)nb * L * grab_words * 4) HIP_TRY(r->grabs.alloc((size_t)nb * L * grab_words * 4));
   HIP_TRY(hipMemsetAsync(r->grabs.p, 0, (size_t)nb * L * grab_words * 4, r->stream));
+  const uint32_t launches_per_batch = r->path_mode ? 1u : L;
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
-    const size_t need = (size_t)2 * ((nb + r->profile_every - 1) / r->profile_every) * L;
+    const size_t need = (size_t)2 * ((nb + r->profile_every - 1) / r->profile_every) * launches_per_batch;
     while (d.kernel_events.size() < need) {
       hipEvent_t e;
       HIP_TRY(hipEventCreate(&e));
@@ -1171,7 +1190,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     FrameSlot& fs = r->slots[k % r->inflight];
     uint32_t* seg = fs.segments.as<uint32_t>();
     uint32_t* meta = seg + 4 * (size_t)r->grid;
-    for (uint32_t b = 0; b < L; ++b) {
+    for (uint32_t b = 0; b < launches_per_batch; ++b) {
       mrt::BounceArgs a{};
       a.width = r->desc.width;
       a.height = r->desc.height;
@@ -1199,9 +1218,11 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.noise_offset = (uint32_t)((int64_t)f - r->noise_first);
       a.radiance = fs.radiance.as<float4>();
       a.stack_spill = fs.spill.as<uint32_t>();
+      a.bounce_counts = cnt + (size_t)k * L;
       const bool timed = profile && (k % r->profile_every) == 0;
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
-      HIP_TRY(launch_bounce(r, a, fs.stream));
+      if (r->path_mode) HIP_TRY(launch_paths(r, a, fs.stream));
+      else HIP_TRY(launch_bounce(r, a, fs.stream));
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
     }
     // accumulateImage for frames f .. f+batch-1, after the previous batch's
