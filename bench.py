@@ -387,7 +387,8 @@ def main():
                      "counter": counter,
                      "limiter": "VALU issue + memory latency of BVH traversal (not HBM bandwidth)",
                      "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),
-                     "kernel": "bounce_kernel", "launches": launches, "timed_launches": timed,
+                     "kernel": "path_kernel (all bounces per launch)" if st["kernel"] == 1 else "bounce_kernel (one launch per bounce)",
+                     "launches": launches, "timed_launches": timed,
                      "avg_launch_ms": round(avg_launch_ms, 4),
                      "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
                      "active_ray_bounces_per_step": int(A / max(1, args.steps))},

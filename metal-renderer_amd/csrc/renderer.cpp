@@ -305,6 +305,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
   r->frame_index = 0;
   r->stats = mrt_stats{};
   r->stats.owned_pixels = r->owned_pixels;
+  r->stats.kernel = r->path_mode ? 1u : 0u;
   return MRT_OK;
 }
 

@@ -3,7 +3,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_extra_${1:-c2}
 mkdir -p $OUT
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY --kernel-include-regex bounce_ -d $OUT -o run -f csv -- python3 bench.py --config ${1:-c2} --steps 2 --warmup 1 --no-cpu-baseline > $OUT/log.txt 2>&1
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY --kernel-include-regex 'bounce_|path_kernel' -d $OUT -o run -f csv -- python3 bench.py --config ${1:-c2} --steps 2 --warmup 1 --no-cpu-baseline > $OUT/log.txt 2>&1
 rc=$?
 tail -3 $OUT/log.txt
 python3 - "$OUT" <<'PY'
@@ -11,7 +11,7 @@ import csv, sys, collections, glob
 agg = collections.defaultdict(float); n = collections.Counter()
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "bounce_" in r["Kernel_Name"]:
+        if "bounce_" in r["Kernel_Name"] or "path_kernel" in r["Kernel_Name"]:
             agg[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
 for k in sorted(agg): print(f"{k:24s} {agg[k]/n[k]:.4g}")
 wc = agg["SQ_WAVE_CYCLES"]

@@ -22,11 +22,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(path, kernel="bounce_"):
+HOT = ("bounce_", "path_kernel")   # the hot kernel: wavefront bounce kernels or the path megakernel
+
+
+def counters(path):
     agg, n = collections.defaultdict(float), collections.Counter()
     meta = {}
     for r in csv.DictReader(open(path)):
-        if kernel not in r["Kernel_Name"]:
+        if not any(k in r["Kernel_Name"] for k in HOT):
             continue
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
         n[r["Counter_Name"]] += 1
@@ -45,7 +48,7 @@ def main(tag="r1", cfg="c2"):
     write, _ = counters(os.path.join(src, "write", "run_counter_collection.csv"))
     sq, _ = counters(os.path.join(src, "sq", "run_counter_collection.csv"))
     clk, _ = counters(os.path.join(src, "clk", "run_counter_collection.csv"))
-    bounce = next(r for r in rows if "bounce_" in r["Name"])
+    bounce = next(r for r in rows if any(k in r["Name"] for k in HOT))
     avg_ns = float(bounce["AverageNs"])
     hbm = (2.0 * fetch["FETCH_SIZE"] + write["WRITE_SIZE"]) * 1024.0
     lines = [f"# rocprofv3 summary — {tag} / {cfg}", "",
@@ -55,7 +58,7 @@ def main(tag="r1", cfg="c2"):
     for r in rows:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                      f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.2f} |")
-    lines += ["", "## bounce_kernel PMC (per launch, averaged)", "",
+    lines += ["", f"## {bounce['Name'][:60]} PMC (per launch, averaged)", "",
               f"* FETCH_SIZE {fetch['FETCH_SIZE']:.0f} KB (×2 gfx950 correction), WRITE_SIZE {write['WRITE_SIZE']:.0f} KB "
               f"→ **HBM traffic {hbm / 1e6:.1f} MB per launch**, {hbm / (avg_ns * 1e-9) / 1e9:.0f} GB/s over the "
               f"average launch ({avg_ns / 1e3:.1f} µs)",
@@ -81,7 +84,7 @@ def main(tag="r1", cfg="c2"):
     with open(os.path.join(out, f"{tag}_{cfg}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(out, f"pmc_{cfg}.json"), "w") as f:
-        json.dump({"tag": tag, "config": cfg, "kernel": "bounce_kernel", "commit": commit,
+        json.dump({"tag": tag, "config": cfg, "kernel": bounce["Name"].split("(")[0].split("::")[-1], "commit": commit,
                    "hbm_bytes_per_launch": round(hbm),
                    "fetch_size_kb": fetch["FETCH_SIZE"], "write_size_kb": write["WRITE_SIZE"],
                    "avg_launch_ns_rocprof": avg_ns, "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
