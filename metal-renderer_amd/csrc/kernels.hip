@@ -113,6 +113,25 @@ __device__ __forceinline__ bool tri_test(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float 
   return true;
 }
 
+// The same arithmetic as tri_test without the early exits (so the same hits,
+// bit for bit), for the leaf loops: the distance range test is left to the
+// caller.  Every operand is needed before the first decision, so the loads of
+// a triangle are all in flight together instead of v0's being issued only
+// after the determinant test passed.
+__device__ __forceinline__ bool tri_bary(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, float& v) {
+  const V3 p = cross(d, e2);
+  const float det = dot(e1, p);
+  const float inv = m_rcp(det);
+  const V3 s = sub(o, v0);
+  const float b1 = dot(s, p) * inv;
+  const V3 q = cross(s, e1);
+  const float b2 = dot(d, q) * inv;
+  t = dot(e2, q) * inv;
+  u = (1.0f - b1) - b2;
+  v = b1;
+  return (det != 0.0f) & (b1 >= 0.0f) & (b1 <= 1.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f);
+}
+
 struct Hit {
   float t, u, v;
   uint32_t prim;
@@ -264,9 +283,9 @@ struct LdsCtx {
   uint32_t mat_base;
   uint32_t light_base;
   uint32_t scratch_base;  // uint32 offset of the per-block scratch
-  uint32_t stack_base;    // uint32 offset of this lane's stack slot 0
-  uint32_t* spill;        // stack entries >= STACK: this lane's column of a global
-  uint32_t spill_stride;  //   [entry][lane] spill area (null when STACK covers the BVH)
+  uint32_t stack_base;    // uint32 offset of the block's stack slot 0 (lane 0's); lanes add threadIdx.x
+  uint32_t* spill;        // stack entries >= STACK: the block's columns of a global [entry][lane]
+  uint32_t spill_stride;  //   spill area (null when STACK covers the BVH); lanes add threadIdx.x
   uint32_t spill_hi;      // BVH8 (two-word entries): offset of the second word's plane in the spill area
 };
 
@@ -376,14 +395,18 @@ __device__ __forceinline__ float4 fetch_light(const DeviceScene& sc, const LdsCt
 template <int STACK>
 __device__ __forceinline__ void stack_push(const LdsCtx& cx, int sp, int32_t v) {
   constexpr int kL = STACK < 0 ? -STACK : STACK;
-  if (STACK > 0 || sp < kL) lds_u32()[cx.stack_base + sp * kBlock] = (uint32_t)v;
-  else cx.spill[(size_t)(sp - kL) * cx.spill_stride] = (uint32_t)v;
+  if (STACK > 0 || sp < kL) lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock] = (uint32_t)v;
+  else cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride] = (uint32_t)v;
 }
 template <int STACK>
 __device__ __forceinline__ int32_t stack_get(const LdsCtx& cx, int sp) {
   constexpr int kL = STACK < 0 ? -STACK : STACK;
-  if (STACK > 0 || sp < kL) return (int32_t)lds_u32()[cx.stack_base + sp * kBlock];
-  return (int32_t)cx.spill[(size_t)(sp - kL) * cx.spill_stride];
+  if (STACK > 0 || sp < kL) return (int32_t)lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock];
+  uint32_t v = cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride];
+  // keeps the two loads apart: merged, they become one flat load whose wait
+  // covers every outstanding global access (the spill stores included)
+  asm("" : "+v"(v));
+  return (int32_t)v;
 }
 
 // Stage the LDS image for `MODE` (every thread of the block calls it);
@@ -405,9 +428,9 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   cx.light_base = cx.mat_base + 2 * M;
   const uint32_t f4 = cx.light_base + 7 * NL;
   cx.scratch_base = 4 * f4;
-  cx.stack_base = cx.scratch_base + ((scratch_u32 + 3) & ~3u) + threadIdx.x;
+  cx.stack_base = cx.scratch_base + ((scratch_u32 + 3) & ~3u);
   cx.spill_stride = gridDim.x * kBlock;
-  cx.spill = spill ? spill + blockIdx.x * kBlock + threadIdx.x : nullptr;
+  cx.spill = spill ? spill + blockIdx.x * kBlock : nullptr;
   cx.spill_hi = sc.max_stack * cx.spill_stride;
   if (MODE != kGlobal) {
     const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes), reinterpret_cast<const float4*>(sc.tris),
@@ -502,6 +525,72 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
   }
 }
 
+// The triangles [first, first + cnt) of a leaf in index order; from global
+// memory two at a time with both triangles' loads issued before either test
+// (one memory round trip per pair).  Nearest (any = false): updates h (ties ->
+// lowest primitive index; (u, v) to uv[0], uv[kBlock] when uv is non-null).
+// Occlusion (any = true): true at the first primitive k != target with
+// (t_k, k) < (h.t, target).
+template <int MODE>
+__device__ __forceinline__ bool leaf_tests(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
+                                           uint32_t first, uint32_t cnt, Hit& h, bool any, uint32_t target,
+                                           uint32_t* uv) {
+  if constexpr (MODE == kAllLds) {   // LDS-resident triangles: one at a time, early-exit test (fewer VGPRs)
+    for (uint32_t k = 0; k < cnt; ++k) {
+      float4 t0, t1, t2;
+      fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
+      const uint32_t prim = fbits(t0.w);
+      float t, u, v;
+      const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v);
+      if (any) {
+        if (hit & (prim != target) & ((t < h.t) | (prim < target))) return true;
+      } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
+        h.found = true;
+        h.t = t;
+        if (uv) {
+          uv[0] = fbits(u);
+          uv[kBlock] = fbits(v);
+        } else {
+          h.u = u;
+          h.v = v;
+        }
+        h.prim = prim;
+      }
+    }
+    return false;
+  }
+  for (uint32_t k = 0; k < cnt; k += 2) {
+    const uint32_t k1 = min(k + 1, cnt - 1);
+    float4 a0, a1, a2, b0, b1, b2;
+    fetch_tri<MODE>(sc, cx, first + k, a0, a1, a2);
+    fetch_tri<MODE>(sc, cx, first + k1, b0, b1, b2);
+    float t[2], u[2], v[2];
+    bool ok[2];
+    ok[0] = tri_bary(o, d, mk(a0), mk(a1), mk(a2), t[0], u[0], v[0]);
+    ok[1] = tri_bary(o, d, mk(b0), mk(b1), mk(b2), t[1], u[1], v[1]) & (k1 != k);
+    const uint32_t prim[2] = {fbits(a0.w), fbits(b0.w)};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool hit = ok[j] & (t[j] >= tmin) & (t[j] <= h.t);
+      if (any) {
+        if (hit & (prim[j] != target) & ((t[j] < h.t) | (prim[j] < target))) return true;
+      } else if (hit & (!h.found | (t[j] < h.t) | (prim[j] < h.prim))) {
+        h.found = true;
+        h.t = t[j];
+        if (uv) {
+          uv[0] = fbits(u[j]);
+          uv[kBlock] = fbits(v[j]);
+        } else {
+          h.u = u[j];
+          h.v = v[j];
+        }
+        h.prim = prim[j];
+      }
+    }
+  }
+  return false;
+}
+
 template <int STACK, int MODE, int WIDTH, bool ANY>
 __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
                                          uint32_t target) {
@@ -523,22 +612,7 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
     while (leaf < 0) {
       const uint32_t lr = ~(uint32_t)leaf;
       const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
-      for (uint32_t k = 0; k < cnt; ++k) {
-        float4 t0, t1, t2;
-        fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
-        const uint32_t prim = fbits(t0.w);
-        float t, u, v;
-        const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v);
-        if (ANY) {
-          if (hit & (prim != target) & ((t < h.t) | (prim < target))) return true;
-        } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
-          h.found = true;
-          h.t = t;
-          h.u = u;
-          h.v = v;
-          h.prim = prim;
-        }
-      }
+      if (leaf_tests<MODE>(sc, cx, o, d, tmin, first, cnt, h, ANY, target, nullptr)) return true;
       leaf = 0;
       if (node < 0) {   // the next node is a leaf too: take it now
         leaf = node;
@@ -565,22 +639,22 @@ template <int STACK>
 __device__ __forceinline__ void stack_push2(const LdsCtx& cx, int sp, uint32_t lo, uint32_t hi) {
   constexpr int kL = STACK < 0 ? -STACK : STACK;
   if (STACK > 0 || sp < kL) {
-    lds_u32()[cx.stack_base + sp * kBlock] = lo;
-    lds_u32()[cx.stack_base + (kL + sp) * kBlock] = hi;
+    lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock] = lo;
+    lds_u32()[cx.stack_base + threadIdx.x + (kL + sp) * kBlock] = hi;
   } else {
-    cx.spill[(size_t)(sp - kL) * cx.spill_stride] = lo;
-    cx.spill[(size_t)(sp - kL) * cx.spill_stride + cx.spill_hi] = hi;
+    cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride] = lo;
+    cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride + cx.spill_hi] = hi;
   }
 }
 template <int STACK>
 __device__ __forceinline__ void stack_get2(const LdsCtx& cx, int sp, uint32_t& lo, uint32_t& hi) {
   constexpr int kL = STACK < 0 ? -STACK : STACK;
   if (STACK > 0 || sp < kL) {
-    lo = lds_u32()[cx.stack_base + sp * kBlock];
-    hi = lds_u32()[cx.stack_base + (kL + sp) * kBlock];
+    lo = lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock];
+    hi = lds_u32()[cx.stack_base + threadIdx.x + (kL + sp) * kBlock];
   } else {
-    lo = cx.spill[(size_t)(sp - kL) * cx.spill_stride];
-    hi = cx.spill[(size_t)(sp - kL) * cx.spill_stride + cx.spill_hi];
+    lo = cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride];
+    hi = cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride + cx.spill_hi];
   }
 }
 
@@ -1450,9 +1524,12 @@ __device__ __forceinline__ bool trav_done(const Trav& tr) { return tr.node == kD
 // one leaf) until every lane still descending holds a leaf, then the parked
 // leaves.  any = occlusion query: stops at the first triangle k != target
 // with (t_k, k) < (h.t, target) and sets `occluded`.
+// uv: when non-null, the nearest hit's barycentrics go to uv[0], uv[kBlock]
+// (the lane's LDS path state) instead of h.u, h.v.
 template <int STACK, int MODE, int WIDTH>
 __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, const RayBox& rb,
-                                           Hit& h, bool any, uint32_t target, bool& occluded, Trav& tr) {
+                                           Hit& h, bool any, uint32_t target, bool& occluded, Trav& tr,
+                                           uint32_t* uv = nullptr) {
   while (tr.node != kDone && tr.node >= 0) {
     tr.node = interior_step<STACK, MODE, WIDTH, false>(sc, cx, tr.node, o, rb, 0.0f, h.t, tr.sp);
     if (tr.node < 0 && tr.leaf == 0) {
@@ -1464,24 +1541,7 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
   while (tr.leaf < 0) {
     const uint32_t lr = ~(uint32_t)tr.leaf;
     const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
-    bool stop = false;
-    for (uint32_t k = 0; k < cnt; ++k) {
-      float4 t0, t1, t2;
-      fetch_tri<MODE>(sc, cx, first + k, t0, t1, t2);
-      const uint32_t prim = fbits(t0.w);
-      float t, u, v;
-      const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), 0.0f, h.t, t, u, v);
-      if (any) {
-        if (hit & (prim != target) & ((t < h.t) | (prim < target))) { stop = true; break; }
-      } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
-        h.found = true;
-        h.t = t;
-        h.u = u;
-        h.v = v;
-        h.prim = prim;
-      }
-    }
-    if (stop) {   // occluded: the query is over
+    if (leaf_tests<MODE>(sc, cx, o, d, 0.0f, first, cnt, h, any, target, uv)) {   // occluded: the query is over
       occluded = true;
       tr.node = kDone;
       tr.leaf = 0;
@@ -1535,7 +1595,7 @@ __global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel
   const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const uint32_t back = (a.bounce % 3u) == 0 ? 0u : ((a.bounce % 3u) == 1 ? 2u : 1u);
   // this lane's parked-state words: after the traversal stack (kLaneStateWords x [word][lane])
-  const uint32_t st_base = cx.stack_base + (uint32_t)(STACK < 0 ? -STACK : STACK) * kBlock;
+  const uint32_t st_base = cx.stack_base + threadIdx.x + (uint32_t)(STACK < 0 ? -STACK : STACK) * kBlock;
 
   // wave-uniform pool of input indices [pool_next, pool_end) of the current grab
   uint32_t pool_next = 0, pool_end = 0;
@@ -1819,7 +1879,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   const uint32_t rlen = ((N + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
   uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
   const uint32_t lane = tid & 63u;
-  uint32_t* const ps = lds_u32() + cx.stack_base + (uint32_t)(STACK < 0 ? -STACK : STACK) * kBlock;
+  uint32_t* const ps = lds_u32() + cx.stack_base + threadIdx.x + (uint32_t)(STACK < 0 ? -STACK : STACK) * kBlock;
 
   uint32_t pool_next = 0, pool_end = 0;   // wave-uniform pool of pixel-sample indices
   bool exhausted = false;
