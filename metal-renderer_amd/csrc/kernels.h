@@ -83,7 +83,7 @@ struct BounceArgs {
   float4* radiance;            // [batch][num_slots] path radiance by owned slot, written once per
                                // owned pixel when its path ends (accumulated by launch_accumulate_frame)
   uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
-                               // [max_stack - stack_entries][grid * 256] uint32 (null if none)
+                               // [grid * 256][max_stack (x2 for BVH8)] uint32 (null if none)
   uint32_t* bounce_counts;     // path kernel: [max_path_length] rays alive at the start of bounce b + 1
 };
 

@@ -284,9 +284,10 @@ struct LdsCtx {
   uint32_t light_base;
   uint32_t scratch_base;  // uint32 offset of the per-block scratch
   uint32_t stack_base;    // uint32 offset of the block's stack slot 0 (lane 0's); lanes add threadIdx.x
-  uint32_t* spill;        // stack entries >= STACK: the block's columns of a global [entry][lane]
-  uint32_t spill_stride;  //   spill area (null when STACK covers the BVH); lanes add threadIdx.x
-  uint32_t spill_hi;      // BVH8 (two-word entries): offset of the second word's plane in the spill area
+  uint32_t* spill;        // stack entries >= STACK: the block's rows of a global [lane][word] spill
+                          //   area (null when STACK covers the BVH); lane threadIdx.x's row
+  uint32_t spill_lane;    //   starts threadIdx.x * spill_lane words in (one word per BVH4 entry,
+                          //   two per BVH8 group entry)
 };
 
 __device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
@@ -392,17 +393,22 @@ __device__ __forceinline__ float4 fetch_light(const DeviceScene& sc, const LdsCt
 
 // STACK = LDS entries per lane; a negative STACK means |STACK| LDS entries
 // plus the global spill area for deeper entries.
+// A lane's spilled words are contiguous: its pushes and pops keep touching
+// the same few cache lines (measured +1.1 % C4, +1.5 % C3 over [entry][lane]).
+__device__ __forceinline__ uint32_t spill_index(const LdsCtx& cx, int w) {
+  return threadIdx.x * cx.spill_lane + (uint32_t)w;
+}
 template <int STACK>
 __device__ __forceinline__ void stack_push(const LdsCtx& cx, int sp, int32_t v) {
   constexpr int kL = STACK < 0 ? -STACK : STACK;
   if (STACK > 0 || sp < kL) lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock] = (uint32_t)v;
-  else cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride] = (uint32_t)v;
+  else cx.spill[spill_index(cx, sp - kL)] = (uint32_t)v;
 }
 template <int STACK>
 __device__ __forceinline__ int32_t stack_get(const LdsCtx& cx, int sp) {
   constexpr int kL = STACK < 0 ? -STACK : STACK;
   if (STACK > 0 || sp < kL) return (int32_t)lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock];
-  uint32_t v = cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride];
+  uint32_t v = cx.spill[spill_index(cx, sp - kL)];
   // keeps the two loads apart: merged, they become one flat load whose wait
   // covers every outstanding global access (the spill stores included)
   asm("" : "+v"(v));
@@ -429,9 +435,8 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   const uint32_t f4 = cx.light_base + 7 * NL;
   cx.scratch_base = 4 * f4;
   cx.stack_base = cx.scratch_base + ((scratch_u32 + 3) & ~3u);
-  cx.spill_stride = gridDim.x * kBlock;
-  cx.spill = spill ? spill + blockIdx.x * kBlock : nullptr;
-  cx.spill_hi = sc.max_stack * cx.spill_stride;
+  cx.spill_lane = (sc.width == 8 ? 2u : 1u) * sc.max_stack;
+  cx.spill = spill ? spill + (size_t)blockIdx.x * kBlock * cx.spill_lane : nullptr;
   if (MODE != kGlobal) {
     const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes), reinterpret_cast<const float4*>(sc.tris),
                             reinterpret_cast<const float4*>(sc.prims), reinterpret_cast<const float4*>(sc.materials),
@@ -642,8 +647,8 @@ __device__ __forceinline__ void stack_push2(const LdsCtx& cx, int sp, uint32_t l
     lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock] = lo;
     lds_u32()[cx.stack_base + threadIdx.x + (kL + sp) * kBlock] = hi;
   } else {
-    cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride] = lo;
-    cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride + cx.spill_hi] = hi;
+    cx.spill[spill_index(cx, 2 * (sp - kL))] = lo;
+    cx.spill[spill_index(cx, 2 * (sp - kL)) + 1] = hi;
   }
 }
 template <int STACK>
@@ -653,8 +658,8 @@ __device__ __forceinline__ void stack_get2(const LdsCtx& cx, int sp, uint32_t& l
     lo = lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock];
     hi = lds_u32()[cx.stack_base + threadIdx.x + (kL + sp) * kBlock];
   } else {
-    lo = cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride];
-    hi = cx.spill[threadIdx.x + (size_t)(sp - kL) * cx.spill_stride + cx.spill_hi];
+    lo = cx.spill[spill_index(cx, 2 * (sp - kL))];
+    hi = cx.spill[spill_index(cx, 2 * (sp - kL)) + 1];
   }
 }
 
@@ -2332,6 +2337,7 @@ hipError_t path_dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t st
   if (sc.width == 8) return hipErrorInvalidValue;
   if (sc.max_stack > stack_entries) {
     if (stack_entries <= 8) return path_dispatch_width<-8>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 12) return path_dispatch_width<-12>(sc, a, grid, grid_out, s);
     if (stack_entries <= 16) return path_dispatch_width<-16>(sc, a, grid, grid_out, s);
     return path_dispatch_width<-32>(sc, a, grid, grid_out, s);
   }

@@ -291,9 +291,9 @@ int alloc_frame_buffers(mrt_renderer* r) {
       for (int p = 0; p < 4; ++p) HIP_TRY(fs.queue[q][p].alloc(r->path_mode ? 0 : slots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
-    // BVH8 group entries are two words: the second plane starts max_stack
-    // entries into the area (kernels.hip LdsCtx::spill_hi)
-    const size_t spill_entries = r->scene->dev.width == 8 ? 2 * (size_t)need : (size_t)(need - r->stack_entries);
+    // spill rows of max_stack words per lane (BVH8 group entries: two words;
+    // kernels.hip LdsCtx::spill_lane)
+    const size_t spill_entries = r->scene->dev.width == 8 ? 2 * (size_t)need : (size_t)need;
     if (need > r->stack_entries && !fs.spill.p) HIP_TRY(fs.spill.alloc(spill_entries * r->grid * 256 * 4));
   }
   if (r->own_image) {
@@ -1087,7 +1087,8 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   if (const char* v = std::getenv("MRT_STACK")) cap = std::max<uint32_t>(8, (uint32_t)std::strtoul(v, nullptr, 0));
   const uint32_t want = std::min(need, cap);
   r->stack_entries = want <= 8 ? 8 : want <= 12 ? 12 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
-  if (need > r->stack_entries) r->stack_entries = r->stack_entries <= 8 ? 8 : r->stack_entries <= 16 ? 16 : 32;   // spill variants
+  if (need > r->stack_entries)   // spill variants: 8 / 12 (path kernel; the wavefront runs 16) / 16 / 32
+    r->stack_entries = r->stack_entries <= 8 ? 8 : r->stack_entries <= 12 ? 12 : r->stack_entries <= 16 ? 16 : 32;
   if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
   if (const char* v = std::getenv("MRT_PROFILE_EVERY"))
     r->profile_every = std::max<uint32_t>(1, (uint32_t)std::strtoul(v, nullptr, 0));
