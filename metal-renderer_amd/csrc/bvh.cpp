@@ -414,7 +414,69 @@ bool emit_bvh8(const std::vector<BuildNode>& bn, const std::vector<Box>& prim_bo
   return true;
 }
 
+// per-axis exponent of a node's quantisation grid: 255 steps of 2^e from lo
+// reach hi (in float, as the kernels compute planes)
+inline int grid_exponent(float lo, float hi) {
+  const double ext = (double)hi - (double)lo;
+  int e = ext > 0.0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
+  e = std::max(-100, std::min(100, e));
+  while (q_plane(lo, e, 255) < hi) ++e;
+  return e;
+}
+
+// outward-rounded 8-bit planes of [clo, chi] on the grid (lo, e), checked in float
+inline bool quantize_span(float lo, int e, float clo, float chi, uint32_t& ql_out, uint32_t& qh_out) {
+  const double sc = std::ldexp(1.0, e);
+  int ql = (int)std::floor(((double)clo - (double)lo) / sc);
+  int qh = (int)std::ceil(((double)chi - (double)lo) / sc);
+  ql = std::max(0, std::min(255, ql));
+  qh = std::max(0, std::min(255, qh));
+  while (ql > 0 && q_plane(lo, e, (uint32_t)ql) > clo) --ql;
+  while (qh < 255 && q_plane(lo, e, (uint32_t)qh) < chi) ++qh;
+  ql_out = (uint32_t)ql;
+  qh_out = (uint32_t)qh;
+  return q_plane(lo, e, (uint32_t)ql) <= clo && q_plane(lo, e, (uint32_t)qh) >= chi;
+}
+
 }  // namespace
+
+bool quantize_bvh4(const std::vector<float>& nodes, uint32_t num_nodes, std::vector<float>& qnodes,
+                   std::string& error) {
+  if (nodes.size() < 32 * (size_t)num_nodes) { error = "quantize_bvh4: not a BVH4 node array"; return false; }
+  qnodes.assign(16 * (size_t)std::max<uint32_t>(1, num_nodes), 0.0f);
+  for (uint32_t k = 0; k < num_nodes; ++k) {
+    const float* n = &nodes[32 * (size_t)k];
+    float* o = &qnodes[16 * (size_t)k];
+    bool live[4];
+    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int c = 0; c < 4; ++c) {
+      live[c] = fbits(n[24 + c]) != (uint32_t)kEmptyChild;
+      if (!live[c]) continue;
+      for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], n[8 * a + c]); hi[a] = std::max(hi[a], n[8 * a + 4 + c]); }
+    }
+    int e[3] = {0, 0, 0};
+    for (int a = 0; a < 3; ++a) {
+      if (lo[a] > hi[a]) lo[a] = hi[a] = 0.0f;   // no live child (not emitted by the builders)
+      e[a] = grid_exponent(lo[a], hi[a]);
+    }
+    uint32_t w[6] = {0, 0, 0, 0, 0, 0};   // qlo.x, qhi.x, qlo.y, qhi.y, qlo.z, qhi.z; byte c = child c
+    for (int c = 0; c < 4; ++c)
+      for (int a = 0; a < 3; ++a) {
+        uint32_t ql = 255, qh = 0;   // empty slot: inverted box
+        if (live[c] && !quantize_span(lo[a], e[a], n[8 * a + c], n[8 * a + 4 + c], ql, qh)) {
+          error = "internal: quantised BVH4 box not conservative";
+          return false;
+        }
+        w[2 * a] |= ql << (8 * c);
+        w[2 * a + 1] |= qh << (8 * c);
+      }
+    o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2];
+    o[3] = bitsf((uint32_t)(e[0] + 128) | ((uint32_t)(e[1] + 128) << 8) | ((uint32_t)(e[2] + 128) << 16));
+    for (int c = 0; c < 4; ++c) o[4 + c] = n[24 + c];
+    for (int i = 0; i < 6; ++i) o[8 + i] = bitsf(w[i]);
+  }
+  return true;
+}
 
 bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indices, uint32_t num_triangles,
                const BvhBuildOptions& opt, BvhResult& out, std::string& error) {

@@ -48,6 +48,13 @@ struct BvhResult {
 bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indices, uint32_t num_triangles,
                const BvhBuildOptions& opt, BvhResult& out, std::string& error);
 
+// Quantised BVH4 (mrt_layout.h, 16 floats per node) from a BVH4's nodes (32
+// floats per node): same node order, refs and leaves; 64-B instead of 128-B
+// node fetches for the path kernel.  Fails if a quantised box would not
+// contain its child's padded box.
+bool quantize_bvh4(const std::vector<float>& nodes, uint32_t num_nodes, std::vector<float>& qnodes,
+                   std::string& error);
+
 inline int32_t leaf_ref(uint32_t first, uint32_t count) {
   return (int32_t)~((first << kLeafCountBits) | (count - 1));
 }

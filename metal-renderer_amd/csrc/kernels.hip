@@ -339,6 +339,19 @@ __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx&
 #pragma unroll
       for (int i = 0; i < 6; ++i) q[i] = p[row[i]];
       q[6] = p[6];
+#ifdef EXP_DOUBLE_LOADS
+      {
+        uint32_t d0, d1, d2, d3, d4, d5, d6;
+        asm volatile("global_load_dword %0, %1, off offset:0" : "=v"(d0) : "v"(p));
+        asm volatile("global_load_dword %0, %1, off offset:16" : "=v"(d1) : "v"(p));
+        asm volatile("global_load_dword %0, %1, off offset:32" : "=v"(d2) : "v"(p));
+        asm volatile("global_load_dword %0, %1, off offset:48" : "=v"(d3) : "v"(p));
+        asm volatile("global_load_dword %0, %1, off offset:64" : "=v"(d4) : "v"(p));
+        asm volatile("global_load_dword %0, %1, off offset:80" : "=v"(d5) : "v"(p));
+        asm volatile("global_load_dword %0, %1, off offset:96" : "=v"(d6) : "v"(p));
+        asm volatile("s_waitcnt vmcnt(0)" : : "v"(d0), "v"(d1), "v"(d2), "v"(d3), "v"(d4), "v"(d5), "v"(d6));
+      }
+#endif
     }
   }
 }
@@ -480,6 +493,76 @@ __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
   return n;
 }
 
+// Quantised BVH4 (width code 5, mrt_layout.h): the node's four rows, from LDS
+// for staged top nodes, else global memory.
+template <int MODE>
+__device__ __forceinline__ void fetch_node4q(const DeviceScene& sc, const LdsCtx& cx, int32_t node, float4 q[4]) {
+  if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = g_lds[4 * node + i];
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 4 * (size_t)node;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = p[i];
+  }
+}
+
+// slab entry distance of quantised plane q on one axis (BVH8 and quantised
+// BVH4): precise ((p + 2^e q) - o) * inv, the plane exactly as the builder
+// checked it; fast fma(q, 2^e inv, (p - o) inv)
+struct Axis8 { float p, s, o, inv, sinv, base; };
+__device__ __forceinline__ float qslab(float qf, const Axis8& a) {
+#if MRT_PRECISE
+  return ((a.p + a.s * qf) - a.o) * a.inv;
+#else
+  return fmaf(qf, a.sinv, a.base);
+#endif
+}
+__device__ __forceinline__ void q_axes(const float4& q0, V3 o, const RayBox& rb, Axis8 ax[3]) {
+  const uint32_t ew = fbits(q0.w);
+  const float pp[3] = {q0.x, q0.y, q0.z}, oo[3] = {o.x, o.y, o.z}, iv[3] = {rb.inv.x, rb.inv.y, rb.inv.z};
+#if !MRT_PRECISE
+  const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
+#endif
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    ax[a].p = pp[a];
+    ax[a].o = oo[a];
+    ax[a].inv = iv[a];
+    ax[a].s = bitsf((((ew >> (8 * a)) & 0xFFu) - 1u) << 23);   // 2^(byte - 128)
+#if !MRT_PRECISE
+    ax[a].sinv = ax[a].s * iv[a];
+    ax[a].base = fmaf(pp[a], iv[a], -oi[a]);
+#endif
+  }
+}
+
+// Box test of the four children of a quantised BVH4 node: entry distances,
+// +inf for a miss or an empty slot.  The near plane of each axis is the hi
+// byte where the direction is negative (slab distances are monotone in the
+// plane), so no planes are paired by min/max.
+__device__ __forceinline__ void box4q(const float4* q, V3 o, const RayBox& rb, float tmin, float tmax, float tn[4]) {
+  Axis8 ax[3];
+  q_axes(q[0], o, rb, ax);
+  const uint32_t sx = fbits(rb.inv.x) >> 31, sy = fbits(rb.inv.y) >> 31, sz = fbits(rb.inv.z) >> 31;
+  const uint32_t lx = fbits(q[2].x), hx = fbits(q[2].y), ly = fbits(q[2].z), hy = fbits(q[2].w);
+  const uint32_t lz = fbits(q[3].x), hz = fbits(q[3].y);
+  const uint32_t nx = sx ? hx : lx, fx = sx ? lx : hx, ny = sy ? hy : ly, fy = sy ? ly : hy;
+  const uint32_t nz = sz ? hz : lz, fz = sz ? lz : hz;
+  const uint32_t ref[4] = {fbits(q[1].x), fbits(q[1].y), fbits(q[1].z), fbits(q[1].w)};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int sh = 8 * k;
+    const float tnx = qslab((float)((nx >> sh) & 0xFFu), ax[0]), tfx = qslab((float)((fx >> sh) & 0xFFu), ax[0]);
+    const float tny = qslab((float)((ny >> sh) & 0xFFu), ax[1]), tfy = qslab((float)((fy >> sh) & 0xFFu), ax[1]);
+    const float tnz = qslab((float)((nz >> sh) & 0xFFu), ax[2]), tfz = qslab((float)((fz >> sh) & 0xFFu), ax[2]);
+    const float tnear = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+    const float tfar = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
+    const bool live = (int32_t)ref[k] != kEmptyChild;
+    tn[k] = (live & (tnear <= tfar)) ? tnear : __builtin_inff();
+  }
+}
+
 // One interior node: returns the next node to visit (nearest hit child, or a
 // popped entry, or kDone); the other hit children are pushed far-to-near.
 template <int STACK, int MODE, int WIDTH, bool ANY>
@@ -500,11 +583,19 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     }
     return right_first ? rr : rl;
   } else {
-    float4 q[7];
-    fetch_node4<MODE>(sc, cx, node, rb, q);
     float t[4];
-    box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0)>(q, o, rb, tmin, tmax, t);
-    int32_t r[4] = {(int32_t)fbits(q[6].x), (int32_t)fbits(q[6].y), (int32_t)fbits(q[6].z), (int32_t)fbits(q[6].w)};
+    int32_t r[4];
+    if constexpr (WIDTH == 5) {   // quantised BVH4: one 64-B line per node
+      float4 q[4];
+      fetch_node4q<MODE>(sc, cx, node, q);
+      box4q(q, o, rb, tmin, tmax, t);
+      r[0] = (int32_t)fbits(q[1].x); r[1] = (int32_t)fbits(q[1].y); r[2] = (int32_t)fbits(q[1].z); r[3] = (int32_t)fbits(q[1].w);
+    } else {
+      float4 q[7];
+      fetch_node4<MODE>(sc, cx, node, rb, q);
+      box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0)>(q, o, rb, tmin, tmax, t);
+      r[0] = (int32_t)fbits(q[6].x); r[1] = (int32_t)fbits(q[6].y); r[2] = (int32_t)fbits(q[6].z); r[3] = (int32_t)fbits(q[6].w);
+    }
     const float inf = __builtin_inff();
     // near-to-far order for occlusion rays too: measured +2.5 % (C2) and
     // +4.5 % (C4) over slot order — near children hold the likely occluders
@@ -683,39 +774,13 @@ __device__ __forceinline__ uint32_t octant_order(uint32_t x, uint32_t oct) {
   return x;
 }
 
-// slab entry distance of quantised plane q on one axis (see mrt_layout.h):
-// precise: ((p + 2^e q) - o) * inv, the plane exactly as the builder checked it;
-// fast: fma(q, 2^e inv, (p - o) inv)
-struct Axis8 { float p, s, o, inv, sinv, base; };
-__device__ __forceinline__ float qslab(float qf, const Axis8& a) {
-#if MRT_PRECISE
-  return ((a.p + a.s * qf) - a.o) * a.inv;
-#else
-  return fmaf(qf, a.sinv, a.base);
-#endif
-}
 
 // Test the 8 children of a node: returns the hit slot mask; tri_bits gets the
 // triangle bits of the hit leaf slots (relative to the node's tri_base).
 __device__ __forceinline__ uint32_t box8(const float4 q[5], V3 o, const RayBox& rb, float tmin, float tmax,
                                          uint32_t& tri_bits) {
-  const uint32_t ew = fbits(q[0].w);
   Axis8 ax[3];
-  const float pp[3] = {q[0].x, q[0].y, q[0].z}, oo[3] = {o.x, o.y, o.z}, iv[3] = {rb.inv.x, rb.inv.y, rb.inv.z};
-#if !MRT_PRECISE
-  const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
-#endif
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    ax[a].p = pp[a];
-    ax[a].o = oo[a];
-    ax[a].inv = iv[a];
-    ax[a].s = bitsf((((ew >> (8 * a)) & 0xFFu) - 1u) << 23);   // 2^(byte - 128)
-#if !MRT_PRECISE
-    ax[a].sinv = ax[a].s * iv[a];
-    ax[a].base = fmaf(pp[a], iv[a], -oi[a]);
-#endif
-  }
+  q_axes(q[0], o, rb, ax);
   // near / far byte planes by the direction's signs (inv < 0: the hi plane is near)
   const uint32_t sx = fbits(rb.inv.x) >> 31, sy = fbits(rb.inv.y) >> 31, sz = fbits(rb.inv.z) >> 31;
   const uint32_t lx0 = fbits(q[2].x), lx1 = fbits(q[2].y), ly0 = fbits(q[2].z), ly1 = fbits(q[2].w);
@@ -2327,8 +2392,9 @@ hipError_t path_dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32
 template <int STACK>
 hipError_t path_dispatch_width(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
                                hipStream_t s) {
-  return sc.width == 4 ? path_dispatch_mode<STACK, 4>(sc, a, grid, grid_out, s)
-                       : path_dispatch_mode<STACK, 2>(sc, a, grid, grid_out, s);
+  return sc.width == 5   ? path_dispatch_mode<STACK, 5>(sc, a, grid, grid_out, s)
+         : sc.width == 4 ? path_dispatch_mode<STACK, 4>(sc, a, grid, grid_out, s)
+                         : path_dispatch_mode<STACK, 2>(sc, a, grid, grid_out, s);
 }
 
 // stack variants as for the bounce kernel; BVH8 scenes are not served here

@@ -93,6 +93,15 @@ static_assert(sizeof(RefLightTriangle) == 100, "RefLightTriangle");
 // Slots follow the octant of the child's centroid relative to the node
 // centre: a ray in octant o (bit a set where direction a < 0) visits slot
 // (k ^ o) k-th, an approximately near-to-far order without sorting.
+//
+// Quantised BVH4 node i = qnodes[4i .. 4i+3] (64 B, one 64-B line; device
+// width code 5, made from a BVH4 by quantize_bvh4 for the path kernel):
+//   [0] = (p.x, p.y, p.z, bits(ex | ey << 8 | ez << 16))   origin, exponent + 128
+//   [1] = bits(ref[0..3])                                   as the BVH4 node's
+//   [2] = (qlo.x[0..3], qhi.x[0..3], qlo.y[0..3], qhi.y[0..3])   one byte per child
+//   [3] = (qlo.z[0..3], qhi.z[0..3], 0, 0)
+// Child plane = p + 2^e * q, rounded outward from the BVH4's padded planes
+// and checked in float as for BVH8; an empty slot has qlo = 255 > qhi = 0.
 constexpr int32_t kEmptyChild = 0x7FFFFFFF;
 constexpr int kLeafCountBits = 4;
 constexpr int kMaxLeafSize = 1 << kLeafCountBits;   // 16
@@ -120,7 +129,7 @@ struct DeviceScene {
   uint32_t num_materials;
   uint32_t num_lights;       // light triangles, excluding the sentinel (SharedData.lightTrianglesCount)
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
-  uint32_t width;            // 2 = BVH2, 4 = BVH4, 8 = compressed BVH8
+  uint32_t width;            // 2 = BVH2, 4 = BVH4, 8 = compressed BVH8, 5 = quantised BVH4 (path kernel)
   uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack)
 };
 
@@ -130,6 +139,6 @@ struct DeviceScene {
 #else
 #define MRT_HD
 #endif
-MRT_HD constexpr uint32_t node_float4s(uint32_t width) { return width == 8 ? 5u : 2u * width; }
+MRT_HD constexpr uint32_t node_float4s(uint32_t width) { return width == 8 ? 5u : width == 5 ? 4u : 2u * width; }
 
 }  // namespace mrt

@@ -144,3 +144,22 @@ def test_frames_in_flight_bitwise(gpu, mrt_mod, monkeypatch, inflight):
         a, b = out[(scene, 1)], out[(scene, inflight)]
         assert np.isfinite(a[0]).all() and a[0][..., :3].max() > 0
         assert a[0].tobytes() == b[0].tobytes() and a[1] == b[1], scene
+
+
+@pytest.mark.parametrize("build", ["precise", "fast"])
+def test_quantised_bvh4_path_kernel_bitwise(gpu, mrt_mod, monkeypatch, build):
+    """MRT_QBVH=1 (opt-in): the path kernel on the 64-B quantised BVH4 nodes
+    renders bitwise like the float BVH4 (outward-rounded boxes only add
+    visits; hits are the triangles' own)."""
+    imgs = []
+    for q in ("0", "1"):
+        monkeypatch.setenv("MRT_QBVH", q)
+        sc = mrt_mod.Scene("cornellbox", procedural_triangles=1 << 16)
+        r = mrt_mod.Renderer(sc, 96, 64, 4, precise=(build == "precise"))
+        assert r.stats()["kernel"] == 1
+        r.draw(2)
+        imgs.append(r.read_image())
+        r.close()
+        sc.close()
+    assert np.isfinite(imgs[0]).all()
+    assert np.array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
