@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--max-path-length", type=int, default=0,
+                   help="override the config's MAX_PATH_LENGTH (e.g. 5 = primary ray + 4 bounces)")
     p.add_argument("--precise", action="store_true", help="time the parity build instead of the fast build")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--bvh", default="sah", choices=["sah", "lbvh", "ploc"],
@@ -235,6 +237,8 @@ def main():
     device = local_rank % ndev   # == local_rank on a full node
     if world > 1:
         dist.init_process_group("gloo")
+    if args.max_path_length:
+        cfg = dict(cfg, L=args.max_path_length, workload=cfg["workload"] + f" (L={args.max_path_length} override)")
     W, H, spp, L = cfg["width"], cfg["height"], cfg["spp"], cfg["L"]
     scene = mrt.Scene(cfg["scene"], resolve_mtl(cfg), procedural_triangles=cfg["procedural"], device=device,
                       bvh_builder={"sah": mrt.BVH_HOST_SAH, "lbvh": mrt.BVH_DEVICE_LBVH,
@@ -368,6 +372,9 @@ def main():
                 (f" + seeded procedural mesh ({cfg['procedural']} tris)" if cfg["procedural"] else "") +
                 ", deterministic noise seed",
         "config": {"workload": cfg["workload"], "width": W, "height": H, "spp": spp, "max_path_length": L,
+                   # MAX_PATH_LENGTH as renderer/Renderer.mm:517 loops it: L ray segments
+                   # per path = the primary ray + (L - 1) bounces
+                   "path_segments": f"primary ray + {L - 1} bounces",
                    "scene": cfg["scene"], "parallelism": (f"tile shard {args.shard_rank} of {shard_count} (one GPU's share)" if args.shard_of else
                                    f"tiles64x{world}" + ((f" + rccl {args.exchange}" + ("" if args.no_overlap or args.exchange == "reduce" else " (overlapped)")
                                                           if args.exchange_backend == "rccl" else " + host/gloo gather") if world > 1 else "")),
