@@ -114,6 +114,15 @@ def _cpu_model():
     return "unknown"
 
 
+def lib_md5(path):
+    import hashlib
+    h = hashlib.md5()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
 def host_threads():
     """The CPUs this process may run on: the affinity mask, capped by the
     worker-pool size the GPU box sets for one GPU's share (OMP_NUM_THREADS=16
@@ -354,7 +363,9 @@ def main():
                        "traffic_over_alg_bytes": round(traffic / max(1, bytes_alg / max(1, launches)), 3),
                        "valu_issue_frac": pmc.get("valu_issue_frac"), "wait_frac": pmc.get("wait_any_frac"),
                        "source": f"profiles/{os.path.basename(pmc_path)} (tag {pmc.get('tag')}, "
-                                 f"commit {pmc.get('commit', 'unrecorded')})"}
+                                 f"commit {pmc.get('commit', 'unrecorded')})",
+                       # the PMC passes measured this very library build (md5 of lib/libmrt.so)
+                       "same_library": (pmc.get("lib_md5") == lib_md5(mrt.LIB_PATH)) if pmc.get("lib_md5") else None}
 
     result = {
         "metric": METRIC,

@@ -15,6 +15,7 @@ import collections
 import csv
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -81,10 +82,15 @@ def main(tag="r1", cfg="c2"):
         commit = None
     lines.append(f"* VALU issue share = 2 x VALU insts / (1024 SIMDs x clock x launch) = "
                  f"{valu_frac if valu_frac is None else round(valu_frac, 3)}")
+    md5_path = os.path.join(src, "lib.md5")
+    lib_md5 = open(md5_path).read().strip() if os.path.exists(md5_path) else None
+    m = re.search(r"(bounce_\w*kernel|path_kernel)<[^>]*>", bounce["Name"])
+    kernel = m.group(0) if m else bounce["Name"][:60]
+    lines.append(f"* measured library: lib/libmrt.so md5 {lib_md5}, repository commit {commit}")
     with open(os.path.join(out, f"{tag}_{cfg}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(out, f"pmc_{cfg}.json"), "w") as f:
-        json.dump({"tag": tag, "config": cfg, "kernel": bounce["Name"].split("(")[0].split("::")[-1], "commit": commit,
+        json.dump({"tag": tag, "config": cfg, "kernel": kernel, "commit": commit, "lib_md5": lib_md5,
                    "hbm_bytes_per_launch": round(hbm),
                    "fetch_size_kb": fetch["FETCH_SIZE"], "write_size_kb": write["WRITE_SIZE"],
                    "avg_launch_ns_rocprof": avg_ns, "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",

@@ -7,6 +7,8 @@ TAG=${1:-r1}; CFG=${2:-c2}; shift 2
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
+# the library these passes measure (bench.py compares it with the one it loads)
+md5sum metal-renderer_amd/lib/libmrt.so | cut -d' ' -f1 > $OUT/lib.md5
 BENCH="python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline $*"
 set -o pipefail
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1; local rc=$?; tail -n 3 $OUT/$name.log; echo "== $name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
