@@ -32,6 +32,22 @@ def test_library_exports_every_declared_symbol(mrt_mod):
     assert mrt_mod.lib().mrt_abi_version() == 4
 
 
+def test_objc_facade_binds_only_declared_symbols(mrt_mod):
+    """integration/objc/Renderer.mm (the drop-in Renderer, not compilable
+    here) calls only functions and flags the C ABI declares, and covers every
+    selector of renderer/Renderer.h:3-8 plus the MTKViewDelegate methods."""
+    src = open(os.path.join(ROOT, "integration", "objc", "Renderer.mm")).read()
+    header = open(os.path.join(ROOT, "include", "mrt.h")).read()
+    called = set(re.findall(r"\b(mrt_\w+)\s*\(", src))
+    assert {"mrt_scene_create", "mrt_renderer_create", "mrt_renderer_resize", "mrt_renderer_draw",
+            "mrt_renderer_display", "mrt_renderer_load_reference", "mrt_renderer_save_image"} <= called
+    assert called <= set(mrt_mod.EXPORTED), called - set(mrt_mod.EXPORTED)
+    for macro in set(re.findall(r"\b(MRT_[A-Z_]+)\b", src)):
+        assert re.search(r"(#define\s+" + macro + r"|^\s*" + macro + r"\s*=)", header, re.M), macro
+    for sel in ("initWithMetalKitView:", "saveCurrentImage", "drawInMTKView:", "drawableSizeWillChange:"):
+        assert sel in src, sel
+
+
 def test_device_count_never_fails(mrt_mod):
     assert mrt_mod.device_count() >= 0
 
