@@ -77,6 +77,8 @@ def parse():
                    help="N=1 only: time rank 0's tiles of an S-way tile split (one GPU's share)")
     p.add_argument("--shard-rank", type=int, default=0,
                    help="with --shard-of: which rank's tiles to render (default 0)")
+    p.add_argument("--no-kernel-timing", action="store_true",
+                   help="no HIP events around the hot kernel's launches (diagnostic: the events' own cost)")
     p.add_argument("--exchange", default="gather", choices=["gather", "reduce"],
                    help="N>1 image exchange: RCCL gather of packed owned tiles (default) or SUM reduce of the image")
     p.add_argument("--no-overlap", action="store_true",
@@ -252,7 +254,7 @@ def main():
     scene = mrt.Scene(cfg["scene"], resolve_mtl(cfg), procedural_triangles=cfg["procedural"], device=device,
                       bvh_builder={"sah": mrt.BVH_HOST_SAH, "lbvh": mrt.BVH_DEVICE_LBVH,
                                    "ploc": mrt.BVH_DEVICE_PLOC}[args.bvh])
-    r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=True,
+    r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=not args.no_kernel_timing,
                      shard_rank=(args.shard_rank if args.shard_of else rank), shard_count=shard_count)
     r.prepare(spp)
 
@@ -351,8 +353,11 @@ def main():
     # issue share.  rocprofv3 --pmc has to wrap the process, so they cannot
     # come from this run; "source" says where they did come from.
     traffic, counter = None, None
+    # (the committed passes measured the whole frame on one GPU: not a tile
+    # share's launches, so they are used only for that geometry)
     pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(pmc_path) and not args.precise:
+    whole_frame = shard_count == 1 and not args.max_path_length
+    if os.path.exists(pmc_path) and not args.precise and (args.pmc or whole_frame):
         with open(pmc_path) as f:
             pmc = json.load(f)
         traffic = pmc.get("hbm_bytes_per_launch")
@@ -405,7 +410,8 @@ def main():
                      "counter": counter,
                      "limiter": "VALU issue + memory latency of BVH traversal (not HBM bandwidth)",
                      "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),
-                     "kernel": "path_kernel (all bounces per launch)" if st["kernel"] == 1 else "bounce_kernel (one launch per bounce)",
+                     "kernel": {1: "path_kernel (all bounces per launch)", 2: "chain_kernel (chained wavefront: all bounces per launch)"}.get(
+                         st["kernel"], "bounce_kernel (one launch per bounce)"),
                      "launches": launches, "timed_launches": timed,
                      "avg_launch_ms": round(avg_launch_ms, 4),
                      "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),

@@ -181,7 +181,8 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
   double kernel_ms;                /* summed durations of the timed launches (MRT_FLAG_PROFILE) */
   uint64_t owned_pixels;
   uint64_t timed_launches;         /* launches behind kernel_ms (every 8th frame's) */
-  uint32_t kernel;                 /* the hot kernel: 0 = wavefront of per-bounce launches, 1 = path megakernel */
+  uint32_t kernel;                 /* the hot kernel: 0 = wavefront of per-bounce launches, 1 = path megakernel,
+                                      2 = chained wavefront (all bounces of a frame batch in one launch) */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);

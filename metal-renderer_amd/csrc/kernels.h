@@ -51,6 +51,27 @@ constexpr uint32_t kSegSlack = 1024;
 constexpr uint32_t kRefillSlack = 2048;   // segment slack of the lane-refill kernel (kernels.hip)
 constexpr uint32_t kMaxSegSlack = kRefillSlack;
 
+// Chained wavefront (chain_kernel): every bounce of a batch in one launch;
+// block j publishes its bounce-b survivor segment into list j % kChainLists
+// of bounce b as soon as its four waves are done with bounce b, and waves
+// that have run out of bounce-b input take bounce-(b+1) rays from published
+// segments (kGrab at a time, per-segment grab counters).  Per batch, zeroed
+// before the launch: lists [L][kChainLists][ceil(G / kChainLists)] uint64
+// entries ((block + 1) | c0 << 16 | c1 << 40, 0 = not yet published), sync
+// words [L][kChainSyncWords] (list heads and fill counters 128 B apart, the
+// count of blocks that published), one error word, and the segment grab
+// counters [L][G][kChainGrabStride].
+constexpr uint32_t kChainLists = 16;
+constexpr uint32_t kChainSyncWords = 1152;
+constexpr uint32_t kChainHeadOff = 0, kChainFillOff = 512, kChainPubOff = 1024;
+constexpr uint32_t kChainGrabStride = 16;
+constexpr uint32_t kChainMaxCount = (1u << 24) - 1;   // c0, c1 field width
+inline size_t chain_list_len(uint32_t G) { return (G + kChainLists - 1) / kChainLists; }
+inline size_t chain_words(uint32_t L, uint32_t G) {   // uint32 words per batch
+  return (size_t)L * kChainLists * chain_list_len(G) * 2 + (size_t)L * kChainSyncWords + 32 +
+         (size_t)L * G * kChainGrabStride;
+}
+
 struct BounceArgs {
   uint32_t width, height;
   uint32_t frame_index;        // SharedData.frameIndex of the batch's first frame
@@ -67,7 +88,13 @@ struct BounceArgs {
   // (left a diffuse surface) to [g*cap, g*cap + c0_g) and its class-1
   // survivors to [g*cap + cap - c1_g, g*cap + cap) of the output queue
   // (cap = chunk + kSegSlack); counts are [c0 of all blocks][c1 of all blocks]
-  uint32_t in_segments;        // bounce > 0: number of input segments (2 x previous grid size)
+  // lane-refill kernel with classes = 4 (MRT_CLASSES=4, measurement of the
+  // per-BSDF re-sort): one class per material type left (diffuse, mirror,
+  // plastic, dielectric); block g owns two segments of cap slots each,
+  // classes 0/1 at the front/back of [2g*cap, 2g*cap + cap) and 2/3 of the
+  // next; counts are [c0 of all blocks][c1 ...][c2 ...][c3 ...]
+  uint32_t classes;            // 2 (default) or 4 (lane-refill kernel only)
+  uint32_t in_segments;        // bounce > 0: number of input segments (classes x previous grid size)
   const uint32_t* in_seg_count;
   const uint32_t* in_chunk;    // previous launch's chunk (segment stride in slots)
   uint32_t* out_seg_count;     // [grid]
@@ -84,7 +111,16 @@ struct BounceArgs {
                                // owned pixel when its path ends (accumulated by launch_accumulate_frame)
   uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
                                // [grid * 256][max_stack (x2 for BVH8)] uint32 (null if none)
-  uint32_t* bounce_counts;     // path kernel: [max_path_length] rays alive at the start of bounce b + 1
+  uint32_t* bounce_counts;     // path / chain kernel: [max_path_length] rays alive at the start of bounce b + 1
+  // chain kernel: the third survivor queue (bounce b reads ring[b % 3] and
+  // writes ring[(b + 1) % 3] of {in_q, out_q, ring2}) and the per-batch
+  // lists / sync words / grab counters (chain_words), error word set when a
+  // wait exceeded its bound (the launch then ends early with a wrong image)
+  RayQueue ring2;
+  uint64_t* chain_list;
+  uint32_t* chain_sync;
+  uint32_t* chain_grab;
+  uint32_t* chain_error;
 };
 
 // running-mean accumulation of one frame over the owned tiles
@@ -122,6 +158,11 @@ struct AccumArgs {
   hipError_t launch_paths(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,            \
                           uint32_t grid, hipStream_t s);                                                  \
   hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                   \
+  /* chained wavefront: all bounces of a batch in one launch over the bounce grid (whole-scene-in-LDS   \
+     BVH2/BVH4 scenes only; hipErrorNotSupported otherwise) */                                            \
+  hipError_t launch_chain(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,            \
+                          uint32_t grid, hipStream_t s);                                                  \
+  bool chain_supported(const DeviceScene& sc, uint32_t stack_entries);                                    \
   /* the scene's LDS staging mode is not "whole scene in LDS": the path kernel is the faster one */      \
   bool path_preferred(const DeviceScene& sc);                                                             \
   /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \

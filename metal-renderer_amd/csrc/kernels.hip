@@ -1039,6 +1039,7 @@ struct PathState {
   float pdf;          // Ray.params.x
   float ior;          // Ray.params.w
   float prevDiffuse;  // Ray.params.y (0 or 1)
+  uint32_t mtype;     // material type of the surface the next ray leaves (set with the next ray)
 };
 struct ShadowRay {
   V3 o, d, L;
@@ -1169,6 +1170,7 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
     s.o = add(hv, mul(hn, kDistanceEpsilon));
     s.pdf = pdf;
     s.prevDiffuse = float(m.type == kDiffuse);
+    s.mtype = m.type;
     s.ior = ior;
     const float q = m_div(bsdf, pdf);
     s.T = mk(s.T.x * (m.kd.x * q), s.T.y * (m.kd.y * q), s.T.z * (m.kd.z * q));
@@ -1233,6 +1235,9 @@ __device__ __forceinline__ uint64_t stamp_real() {
       e_[4] = st_work; e_[5] = st_asum; e_[6] = st_amax; e_[7] = st_grab - st_ab; \
       for (int k_ = 0; k_ < 5; ++k_) e_[8 + k_] = st_acc[k_]; e_[13] = st_entry; } } } while (0)
 #define STAMP_ENTRY() const uint64_t st_entry = stamp_real()
+struct StampRef { uint64_t* acc; uint64_t* prev; };   // a kernel's phase accumulators, for a callee
+#define STAMP_REF() StampRef{st_acc, &st_prev}
+#define STAMP_AT(r, k) do { const uint64_t t_ = stamp_now(); (r).acc[k] += t_ - *(r).prev; *(r).prev = t_; } while (0)
 #define STAMP_ATOMIC_BEGIN() do { st_ab = stamp_real(); } while (0)
 #define STAMP_EXIT(got) do { st_why = (got) == 0xFFFFFFFEu ? 2u : 1u; } while (0)
 #define STAMP_GRAB() do { st_grab = stamp_real(); st_asum += st_grab - st_ab; \
@@ -1248,6 +1253,9 @@ __device__ __forceinline__ uint64_t stamp_real() {
 #define STAMP_WORK() do {} while (0)
 #define STAMP_ATOMIC_BEGIN() do {} while (0)
 #define STAMP_ENTRY() do {} while (0)
+struct StampRef {};
+#define STAMP_REF() StampRef{}
+#define STAMP_AT(r, k) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -1297,6 +1305,134 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n
   return total;
 }
 
+// One wave iteration of the fused bounce: up to 64 rays of bounce `bounce`.
+// Each active lane generates its camera ray (bounce 0: `idx` = the launch's
+// dense index = global slot) or loads its ray from `slot` of `in_q`, finds
+// the nearest hit, shades it (NEE shadow ray, MIS emission, next ray), writes
+// the radiance of a path that ends here, appends a survivor to the block's
+// output segment [out_base, out_base + cap) of `out_q` through the LDS
+// cursors (class 0 = left a diffuse surface, from the front; class 1 from
+// the back) and traces the shadow ray.  Returns the survivors written.
+// Used by bounce_kernel (one launch per bounce) and chain_kernel (all
+// bounces of a batch in one launch).
+template <int STACK, int MODE, int WIDTH>
+__device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const LdsCtx& cx, const BounceArgs& a,
+                                               uint32_t bounce, bool active, uint32_t idx, uint32_t slot,
+                                               const RayQueue& in_q, const RayQueue& out_q, uint32_t* cursor,
+                                               uint32_t out_base, uint32_t cap, uint64_t lanes_below,
+                                               StampRef st) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool last = (bounce + 1 == a.max_path_length);
+  // -- phase 0: generate (bounce 0) or load (SoA queue planes 0-1) the ray
+  PathState s;
+  uint32_t tag = 0;   // tag = global owned slot | prevDiffuse << 31
+  if (active) {
+    if (bounce == 0) {
+      // frame fj of the batch (num_slots is a multiple of 4096: waves never
+      // straddle frames, so fj is wave-uniform)
+      const uint32_t fj = a.batch == 1u ? 0u : __builtin_amdgcn_readfirstlane(idx / a.num_slots);
+      uint32_t x, y;
+      slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+      active = (x < a.width) && (y < a.height);
+      if (active) {
+        tag = idx;
+        const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
+        camera_ray(x, y, a.width, a.height, ns, s.o, s.d);
+      }
+    } else {
+      // planes 2-3 (throughput, pdf, radiance, ior) are loaded after the
+      // traversal: they are not needed there, and keeping them out of the
+      // traversal's live set saves 8 VGPRs
+      const float4 q0 = in_q.plane[0][slot], q1 = in_q.plane[1][slot];
+      s.o = mk(q0);
+      tag = fbits(q0.w);
+      s.d = mk(q1);
+      s.prevDiffuse = (tag >> 31) ? 1.0f : 0.0f;
+    }
+  }
+  STAMP_AT(st, 0);
+  // -- phase 1: nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
+  Hit h;
+  h.found = false;
+  if (active) h = trace_nearest<STACK, MODE, WIDTH>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+  STAMP_AT(st, 1);
+  // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
+  //    near hit ends the path (:122-126)
+  const uint32_t gslot = tag & 0x7FFFFFFFu;
+  if (active) {
+    if (bounce == 0) {
+      s.T = mk(1.0f, 1.0f, 1.0f);
+      s.R = mk(0.0f, 0.0f, 0.0f);
+      s.pdf = 1.0f;
+      s.prevDiffuse = 0.0f;
+      s.ior = 1.00029f;
+    } else {
+      const float4 q2 = in_q.plane[2][slot], q3 = in_q.plane[3][slot];
+      s.T = mk(q2);
+      s.pdf = q2.w;
+      s.R = mk(q3);
+      s.ior = q3.w;
+    }
+  }
+  const bool hit_ok = active && h.found && !(h.t < kDistanceEpsilon);
+  ShadowRay sh;
+  sh.valid = false;
+  if (hit_ok) {
+    const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;   // frame in batch
+    uint32_t x, y;
+    slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+    const uint32_t back = (bounce % 3u) == 0 ? 0u : ((bounce % 3u) == 1 ? 2u : 1u);   // uniform
+    const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, bounce, a.frame_index + fj)];
+    if (a.debug & 2u) {   // ablation: no shading, reflect back along the ray
+      s.o = add(s.o, mul(s.d, h.t * 0.999f));
+      s.d = mk(-s.d.x, -s.d.y, -s.d.z);
+    } else {
+      shade_hit<MODE>(sc, cx, h, s, ns, bounce, a.max_path_length, !last, sh);
+    }
+  }
+  STAMP_AT(st, 2);
+  // -- phase 3: paths that end here (miss, near hit, last bounce: none of
+  //    them carries a shadow ray) go to accumulateImage (:233-249);
+  //    survivors are compacted into this block's segment of the next queue.
+  //    Planes 0-2 are written before the shadow traversal so the next ray
+  //    is not live across it; plane 3 (radiance, ior) after it.
+  if (active && (!hit_ok || last)) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
+  const bool alive = hit_ok && !last;
+  // re-sort by material between bounces: survivors that left a diffuse
+  // surface (class 0) fill the block's segment from the front, the others
+  // (mirror / plastic / dielectric: specular and refracted rays) from the
+  // back; the next bounce reads all class-0 runs first, so its waves see
+  // rays of one class (MRT_DEBUG bit 16: no partition)
+  const bool cls1 = (s.prevDiffuse == 0.0f) && !(a.debug & 16u);
+  const uint64_t mask0 = __ballot(alive && !cls1), mask1 = __ballot(alive && cls1);
+  uint32_t o = 0, wrote = 0;
+  if (mask0 | mask1) {
+    uint32_t w0 = 0, w1 = 0;
+    if (lane == 0) {
+      if (mask0) w0 = atomicAdd(&cursor[0], (uint32_t)__popcll(mask0));
+      if (mask1) w1 = atomicAdd(&cursor[1], (uint32_t)__popcll(mask1));
+    }
+    w0 = __shfl(w0, 0);
+    w1 = __shfl(w1, 0);
+    o = cls1 ? out_base + cap - 1u - (w1 + (uint32_t)__popcll(mask1 & lanes_below))
+             : out_base + w0 + (uint32_t)__popcll(mask0 & lanes_below);
+    if (alive && !(a.debug & 4u)) {
+      out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
+      out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
+      out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
+    }
+    wrote = (uint32_t)__popcll(mask0 | mask1);
+  }
+  STAMP_AT(st, 3);
+  // -- phase 4: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
+  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE, WIDTH>(sc, cx, sh.o, sh.d, sh.target))) {
+    s.R = add(s.R, sh.L);
+  }
+  if (alive && !(a.debug & 4u)) out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
+  STAMP_AT(st, 4);
+  return wrote;
+}
+
 template <int STACK, int MODE, int WIDTH>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
@@ -1340,7 +1476,6 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   uint32_t static_base = blockIdx.x * kBlock + (tid & ~63u);
 
   const uint32_t lane = tid & 63u;
-  const bool last = (a.bounce + 1 == a.max_path_length);
   const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
   STAMP_DECL();
@@ -1389,27 +1524,10 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     }
     uint32_t wrote = 0;
     for (uint32_t it = 0; it < niter; ++it) {
-    const uint32_t base = start + it * 64u;
-    STAMP_BEGIN();
-    // -- phase 0: generate (bounce 0) or load (SoA queue planes 0-1) the ray
-    const uint32_t idx = base + lane;
-    bool active = idx < end;
-    PathState s;
-    uint32_t tag = 0, slot = 0;   // tag = global owned slot | prevDiffuse << 31
-    if (active) {
-      if (a.bounce == 0) {
-        // frame fj of the batch (num_slots is a multiple of 4096: waves never
-        // straddle frames, so fj is wave-uniform)
-        const uint32_t fj = a.batch == 1u ? 0u : __builtin_amdgcn_readfirstlane(idx / a.num_slots);
-        uint32_t x, y;
-        slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
-        active = (x < a.width) && (y < a.height);
-        if (active) {
-          tag = idx;
-          const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
-          camera_ray(x, y, a.width, a.height, ns, s.o, s.d);
-        }
-      } else {
+      const uint32_t idx = start + it * 64u + lane;
+      bool active = idx < end;
+      uint32_t slot = 0;
+      if (active && a.bounce != 0) {
         uint32_t lo = 0, hi = nseg;   // last j with seg[j] <= idx
         while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
         // segments [0, G): class 0 from the start of block j's range;
@@ -1417,96 +1535,10 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
         const uint32_t g_in = nseg >> 1;
         slot = lo < g_in ? lo * in_chunk + (idx - seg[lo])
                          : (lo - g_in) * in_chunk + in_chunk - (seg[lo + 1] - seg[lo]) + (idx - seg[lo]);
-        // planes 2-3 (throughput, pdf, radiance, ior) are loaded after the
-        // traversal: they are not needed there, and keeping them out of the
-        // traversal's live set saves 8 VGPRs
-        const float4 q0 = a.in_q.plane[0][slot], q1 = a.in_q.plane[1][slot];
-        s.o = mk(q0);
-        tag = fbits(q0.w);
-        s.d = mk(q1);
-        s.prevDiffuse = (tag >> 31) ? 1.0f : 0.0f;
       }
-    }
-    STAMP(0);
-    // -- phase 1: nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
-    Hit h;
-    h.found = false;
-    if (active) h = trace_nearest<STACK, MODE, WIDTH>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
-    STAMP(1);
-    // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
-    //    near hit ends the path (:122-126)
-    const uint32_t gslot = tag & 0x7FFFFFFFu;
-    if (active) {
-      if (a.bounce == 0) {
-        s.T = mk(1.0f, 1.0f, 1.0f);
-        s.R = mk(0.0f, 0.0f, 0.0f);
-        s.pdf = 1.0f;
-        s.prevDiffuse = 0.0f;
-        s.ior = 1.00029f;
-      } else {
-        const float4 q2 = a.in_q.plane[2][slot], q3 = a.in_q.plane[3][slot];
-        s.T = mk(q2);
-        s.pdf = q2.w;
-        s.R = mk(q3);
-        s.ior = q3.w;
-      }
-    }
-    const bool hit_ok = active && h.found && !(h.t < kDistanceEpsilon);
-    ShadowRay sh;
-    sh.valid = false;
-    if (hit_ok) {
-      const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;   // frame in batch
-      uint32_t x, y;
-      slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
-      const uint32_t back = (a.bounce % 3u) == 0 ? 0u : ((a.bounce % 3u) == 1 ? 2u : 1u);   // uniform
-      const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, a.bounce, a.frame_index + fj)];
-      if (a.debug & 2u) {   // ablation: no shading, reflect back along the ray
-        s.o = add(s.o, mul(s.d, h.t * 0.999f));
-        s.d = mk(-s.d.x, -s.d.y, -s.d.z);
-      } else {
-        shade_hit<MODE>(sc, cx, h, s, ns, a.bounce, a.max_path_length, !last, sh);
-      }
-    }
-    STAMP(2);
-    // -- phase 3: paths that end here (miss, near hit, last bounce: none of
-    //    them carries a shadow ray) go to accumulateImage (:233-249);
-    //    survivors are compacted into this block's segment of the next queue.
-    //    Planes 0-2 are written before the shadow traversal so the next ray
-    //    is not live across it; plane 3 (radiance, ior) after it.
-    if (active && (!hit_ok || last)) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
-    const bool alive = hit_ok && !last;
-    // re-sort by material between bounces: survivors that left a diffuse
-    // surface (class 0) fill the block's segment from the front, the others
-    // (mirror / plastic / dielectric: specular and refracted rays) from the
-    // back; the next launch reads all class-0 segments first, so its waves
-    // see rays of one class (MRT_DEBUG bit 16: no partition)
-    const bool cls1 = (s.prevDiffuse == 0.0f) && !(a.debug & 16u);
-    const uint64_t mask0 = __ballot(alive && !cls1), mask1 = __ballot(alive && cls1);
-    uint32_t o = 0;
-    if (mask0 | mask1) {
-      uint32_t w0 = 0, w1 = 0;
-      if (lane == 0) {
-        if (mask0) w0 = atomicAdd(&s_cursor[0], (uint32_t)__popcll(mask0));
-        if (mask1) w1 = atomicAdd(&s_cursor[1], (uint32_t)__popcll(mask1));
-      }
-      w0 = __shfl(w0, 0);
-      w1 = __shfl(w1, 0);
-      o = cls1 ? out_base + cap - 1u - (w1 + (uint32_t)__popcll(mask1 & lanes_below))
-               : out_base + w0 + (uint32_t)__popcll(mask0 & lanes_below);
-      if (alive && !(a.debug & 4u)) {
-        a.out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
-        a.out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
-        a.out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
-      }
-      wrote += (uint32_t)__popcll(mask0 | mask1);
-    }
-    STAMP(3);
-    // -- phase 4: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
-    if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE, WIDTH>(sc, cx, sh.o, sh.d, sh.target))) {
-      s.R = add(s.R, sh.L);
-    }
-    if (alive && !(a.debug & 4u)) a.out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
-    STAMP(4);
+      STAMP_BEGIN();
+      wrote += bounce_wave<STACK, MODE, WIDTH>(sc, cx, a, a.bounce, active, idx, slot, a.in_q, a.out_q, s_cursor,
+                                               out_base, cap, lanes_below, STAMP_REF());
     }
     STAMP_WORK();
     if (dynamic && lane == 0) atomicSub(&s_res, kGrab - wrote);
@@ -1522,6 +1554,195 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Chained wavefront: every bounce of a frame batch in ONE launch over the
+// persistent bounce grid (whole-scene-in-LDS scenes, the C1/C2 class).
+//
+// bounce_kernel ends each bounce at a launch boundary: the last grabs drain
+// at falling occupancy, the next launch stages the scene and scans the
+// segment counts again — about 60-110 us per launch, measured on one GPU's
+// 1/8 tile share of C2 (bounce launches of 0.35-1 ms).  Here a wave that
+// finds no bounce-b input left goes straight on to bounce b+1 and takes its
+// rays from the survivor segments of blocks that have already finished
+// bounce b, so the drain of bounce b overlaps bounce b+1 and only the last
+// bounce drains.
+//
+// Hand-off (cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md
+// "inter-workgroup visibility"): every wave of block j waits for its own
+// stores (s_waitcnt vmcnt(0)) before adding to the block's LDS done count;
+// the wave whose add is last releases at agent scope (L2 write-back) and then
+// publishes (j, c0, c1) with one relaxed agent-scope 8-B store into list
+// j % kChainLists of bounce b.  A consumer polls the entry relaxed, and before
+// its first load from a newly taken segment runs an agent-scope acquire.
+// Segments are taken kGrab rays at a time through per-segment grab counters;
+// the lists' heads only move past exhausted entries.
+//
+// Queues: a ring of three — bounce b reads ring[b % 3] and writes
+// ring[(b + 1) % 3], the queue bounce b - 2 read; a wave starts bounce b >= 2
+// only after every block has published bounce b - 2 (it has then finished
+// reading it).  Waiting is bounded (~2 s of s_memrealtime): on expiry the
+// wave sets chain_error and gives up (the host reports an error).  Every
+// block must be resident at once (the grid is the bounce grid: every resident
+// block slot, one launch at a time — frames in flight keep bounce_kernel).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kChainMaxL = 64;
+constexpr uint64_t kChainWaitTicks = 200000000ull;   // s_memrealtime is 100 MHz: 2 s
+
+__device__ __forceinline__ RayQueue ring_queue(const BounceArgs& a, uint32_t k) {
+  return k == 0 ? a.in_q : (k == 1 ? a.out_q : a.ring2);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int STACK, int MODE, int WIDTH>
+__global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void chain_kernel(DeviceScene sc, BounceArgs a) {
+  __shared__ uint32_t s_res[kChainMaxL], s_cur[kChainMaxL][2], s_done[kChainMaxL], s_lclosed[kChainMaxL];
+  __shared__ uint32_t s_closed;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t G = gridDim.x, g = blockIdx.x;
+  const uint32_t L = a.max_path_length;
+  const LdsCtx cx = stage_lds<MODE>(sc, 0, a.stack_spill);
+  for (uint32_t i = tid; i < L; i += kBlock) { s_res[i] = 0; s_cur[i][0] = s_cur[i][1] = 0; s_done[i] = 0; s_lclosed[i] = 0; }
+  if (tid == 0) s_closed = 0;
+  __syncthreads();
+
+  // one capacity for every bounce: survivors of any bounce <= N0
+  const uint32_t N0 = a.num_slots * a.batch;
+  const uint32_t chunk = ((N0 + G - 1) / G + kBlock - 1) / kBlock * kBlock;
+  const uint32_t cap = chunk + kSegSlack;
+  const uint32_t out_base = g * cap;
+  const uint32_t rlen = ((N0 + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
+  const uint32_t list_len = (G + kChainLists - 1) / kChainLists;
+  const uint32_t home = g % kChainLists;   // blocks j, j + 8 share an XCD: list g % 16 holds same-XCD segments
+  const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t cur_range = g % kGrabRanges, ranges_left = kGrabRanges;
+  uint32_t acq_seg = 0xFFFFFFFFu;   // the segment this wave last acquired
+  bool failed = false;               // a bounded wait expired (wave-uniform)
+
+  STAMP_DECL();   // stamp builds: phase cycles accumulate but are not flushed for this kernel
+  const StampRef st = STAMP_REF();
+  for (uint32_t b = 0; b < L && !failed; ++b) {
+    const RayQueue in_q = ring_queue(a, b % 3u), out_q = ring_queue(a, (b + 1) % 3u);
+    // ring: bounce b writes the queue bounce b - 2 read
+    if (b >= 2) {
+      uint32_t ok = 1;
+      if (lane == 0) {
+        const uint32_t* pub = a.chain_sync + (size_t)(b - 2) * kChainSyncWords + kChainPubOff;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (ld_agent(pub) < G) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) { ok = 0; break; }
+          __builtin_amdgcn_s_sleep(4);
+        }
+      }
+      if (!__builtin_amdgcn_readfirstlane(ok)) { failed = true; break; }
+    }
+    const uint32_t* lsync = a.chain_sync + (size_t)(b ? b - 1 : 0) * kChainSyncWords;
+    const uint64_t* lists = a.chain_list + (size_t)(b ? b - 1 : 0) * kChainLists * list_len;
+    uint32_t* lheads = const_cast<uint32_t*>(lsync) + kChainHeadOff;
+    uint32_t cur_list = home;
+    for (;;) {
+      // reserve kGrab output slots of this block's bounce-b segment, then take
+      // up to kGrab rays: bounce 0 from the launch's grab ranges, later
+      // bounces from a published segment of bounce b - 1
+      uint32_t got = 0xFFFFFFFFu, gend = 0, sj = 0, sc0 = 0, sn = 0, werr = 0;
+      if (lane == 0) {
+        if (atomicAdd(&s_res[b], kGrab) + kGrab <= cap) {
+          if (b == 0) {
+            while (ranges_left) {
+              const uint32_t r0 = cur_range * rlen;
+              if (r0 < N0 && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
+                const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
+                if (i < rlen && r0 + i < N0) { got = r0 + i; gend = min(N0, r0 + rlen); break; }
+                atomicOr(&s_closed, 1u << cur_range);
+              }
+              cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
+              --ranges_left;
+            }
+          } else {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+              bool pending = false;
+              for (uint32_t t = 0; t < kChainLists && got == 0xFFFFFFFFu; ++t) {
+                const uint32_t r = cur_list;
+                const uint32_t size_r = G > r ? (G - r + kChainLists - 1) / kChainLists : 0u;
+                if (!(__hip_atomic_load(&s_lclosed[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << r))) {
+                  uint32_t pidx = ld_agent(lheads + r * 32u);
+                  for (;;) {
+                    if (pidx >= size_r) { atomicOr(&s_lclosed[b], 1u << r); break; }   // every entry exhausted
+                    const uint64_t e = ld_agent64(lists + (size_t)r * list_len + pidx);
+                    if (e == 0) { pending = true; break; }                                 // not yet published
+                    const uint32_t j = (uint32_t)(e & 0xFFFFu) - 1u;
+                    const uint32_t c0 = (uint32_t)(e >> 16) & kChainMaxCount, c1 = (uint32_t)(e >> 40);
+                    const uint32_t i = atomicAdd(a.chain_grab + ((size_t)(b - 1) * G + j) * kChainGrabStride, kGrab);
+                    if (i < c0 + c1) { got = i; gend = c0 + c1; sj = j; sc0 = c0; sn = c0 + c1; break; }
+                    atomicMax(lheads + r * 32u, pidx + 1u);
+                    ++pidx;
+                  }
+                }
+                if (got == 0xFFFFFFFFu) cur_list = cur_list + 1 == kChainLists ? 0u : cur_list + 1;
+              }
+              if (got != 0xFFFFFFFFu || !pending) break;
+              if (__builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) { werr = 1; break; }
+              __builtin_amdgcn_s_sleep(2);
+            }
+          }
+          if (got == 0xFFFFFFFFu) atomicSub(&s_res[b], kGrab);   // input exhausted
+        } else {
+          got = 0xFFFFFFFEu;   // the block's bounce-b output segment is full
+        }
+      }
+      got = __builtin_amdgcn_readfirstlane(got);
+      if (__builtin_amdgcn_readfirstlane(werr)) { failed = true; break; }
+      if (got >= 0xFFFFFFFEu) break;
+      gend = __builtin_amdgcn_readfirstlane(gend);
+      sj = __builtin_amdgcn_readfirstlane(sj);
+      sc0 = __builtin_amdgcn_readfirstlane(sc0);
+      sn = __builtin_amdgcn_readfirstlane(sn);
+      cur_range = __builtin_amdgcn_readfirstlane(cur_range);
+      ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
+      cur_list = __builtin_amdgcn_readfirstlane(cur_list);
+      if (b > 0 && sj != acq_seg) {   // first rays of a newly taken segment
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        acq_seg = sj;
+      }
+      const uint32_t gend_c = min(gend, got + kGrab);
+      uint32_t wrote = 0;
+      for (uint32_t it = 0; it < kGrab / 64u; ++it) {
+        const uint32_t off = got + it * 64u + lane;
+        const bool active = off < gend_c;
+        // segment sj: class 0 at [sj*cap, sj*cap + c0), class 1 at the end of its range
+        const uint32_t slot = off < sc0 ? sj * cap + off : sj * cap + cap - (sn - sc0) + (off - sc0);
+        wrote += bounce_wave<STACK, MODE, WIDTH>(sc, cx, a, b, active, off, slot, in_q, out_q, s_cur[b], out_base,
+                                                 cap, lanes_below, st);
+      }
+      if (lane == 0) atomicSub(&s_res[b], kGrab - wrote);
+    }
+    if (failed || b + 1 == L) break;
+    // this wave is done with bounce b: its stores first, then the block's
+    // last wave releases and publishes the block's segment
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0 && atomicAdd(&s_done[b], 1u) == kBlock / 64u - 1u) {
+      const uint32_t c0 = s_cur[b][0], c1 = s_cur[b][1];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint32_t* sync = a.chain_sync + (size_t)b * kChainSyncWords;
+      const uint32_t r = g % kChainLists;
+      const uint32_t pos = atomicAdd(sync + kChainFillOff + r * 32u, 1u);
+      __hip_atomic_store(a.chain_list + ((size_t)b * kChainLists + r) * list_len + pos,
+                         (uint64_t)(g + 1u) | ((uint64_t)c0 << 16) | ((uint64_t)c1 << 40), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(sync + kChainPubOff, 1u);
+      if (c0 + c1) atomicAdd(a.bounce_counts + b, c0 + c1);
+    }
+  }
+  if (failed && lane == 0) atomicOr(a.chain_error, 1u);
+}
 
 // ---------------------------------------------------------------------------
 // Lane-refill bounce kernel (global-memory scenes: kTopLds / kGlobal).
@@ -1605,13 +1826,14 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
 template <int STACK, int MODE, int WIDTH>
 __global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
-  __shared__ uint32_t s_cursor[2], s_res, s_closed;
+  __shared__ uint32_t s_cursor[4], s_res, s_closed;
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
+  const uint32_t ncls = a.classes == 4u ? 4u : 2u;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
   const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1, a.stack_spill);
   uint32_t* seg = lds_u32() + cx.scratch_base;
-  if (tid == 0) s_cursor[0] = s_cursor[1] = s_res = s_closed = 0;
+  if (tid == 0) s_cursor[0] = s_cursor[1] = s_cursor[2] = s_cursor[3] = s_res = s_closed = 0;
   uint32_t N, in_chunk = 0;
   if (a.bounce == 0) {
     N = a.num_slots * a.batch;
@@ -1634,7 +1856,7 @@ __global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel
   // written more than `chunk` survivors, so not every block can stop while
   // input remains
   const uint32_t cap = chunk + kRefillSlack;
-  const uint32_t out_base = blockIdx.x * cap;
+  const uint32_t out_base = blockIdx.x * (ncls >> 1) * cap;
   const uint32_t rlen = ((N + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
   uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
   const uint32_t lane = tid & 63u;
@@ -1709,9 +1931,11 @@ __global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel
         } else {
           uint32_t lo = 0, hi = nseg;
           while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
-          const uint32_t g_in = nseg >> 1;
-          aux1 = lo < g_in ? lo * in_chunk + (idx - seg[lo])
-                           : (lo - g_in) * in_chunk + in_chunk - (seg[lo + 1] - seg[lo]) + (idx - seg[lo]);
+          // segment lo = class c of block j: c even from the front of the
+          // block's (c >> 1)-th cap-slot segment, c odd from its back
+          const uint32_t g_in = nseg / ncls, c = lo / g_in, j = lo - c * g_in;
+          const uint32_t sbase = (j * (ncls >> 1) + (c >> 1)) * in_chunk;
+          aux1 = (c & 1u) ? sbase + in_chunk - (seg[lo + 1] - seg[lo]) + (idx - seg[lo]) : sbase + (idx - seg[lo]);
           const float4 q0 = a.in_q.plane[0][aux1], q1 = a.in_q.plane[1][aux1];
           ro = mk(q0);
           aux0 = fbits(q0.w);
@@ -1815,20 +2039,29 @@ __global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel
       }
       // survivors -> this block's segment of the next queue (material classes)
       const bool alive = shade_now && hit_ok && !last;
-      const bool cls1 = (s.prevDiffuse == 0.0f) && !(a.debug & 16u);
-      const uint64_t mask0 = __ballot(alive && !cls1), mask1 = __ballot(alive && cls1);
+      // class: 2 classes = left a diffuse surface or not; 4 = the material
+      // type left (MRT_DEBUG bit 16: everything in class 0)
+      const uint32_t cls = (a.debug & 16u) ? 0u : ncls == 4u ? s.mtype : (s.prevDiffuse == 0.0f ? 1u : 0u);
+      uint64_t mask[4];
+#pragma unroll
+      for (uint32_t c = 0; c < 4; ++c) mask[c] = (c < ncls) ? __ballot(alive && cls == c) : 0ull;
       uint32_t oslot = 0;
-      if (mask0 | mask1) {
-        uint32_t w0 = 0, w1 = 0;
+      if (mask[0] | mask[1] | mask[2] | mask[3]) {
+        uint32_t w[4] = {0, 0, 0, 0};
         if (lane == 0) {
-          if (mask0) w0 = atomicAdd(&s_cursor[0], (uint32_t)__popcll(mask0));
-          if (mask1) w1 = atomicAdd(&s_cursor[1], (uint32_t)__popcll(mask1));
+#pragma unroll
+          for (uint32_t c = 0; c < 4; ++c)
+            if (mask[c]) w[c] = atomicAdd(&s_cursor[c], (uint32_t)__popcll(mask[c]));
         }
-        w0 = __shfl(w0, 0);
-        w1 = __shfl(w1, 0);
+        uint32_t mine = 0, before = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) {
+          const uint32_t wc = __shfl(w[c], 0);
+          if (cls == c) { mine = wc; before = (uint32_t)__popcll(mask[c] & lanes_below); }
+        }
         if (alive) {
-          oslot = cls1 ? out_base + cap - 1u - (w1 + (uint32_t)__popcll(mask1 & lanes_below))
-                       : out_base + w0 + (uint32_t)__popcll(mask0 & lanes_below);
+          const uint32_t sb = out_base + (cls >> 1) * cap;
+          oslot = (cls & 1u) ? sb + cap - 1u - (mine + before) : sb + mine + before;
           a.out_q.plane[0][oslot] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
           a.out_q.plane[1][oslot] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
           a.out_q.plane[2][oslot] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
@@ -1877,9 +2110,11 @@ __global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel
   }
   __syncthreads();
   if (tid == 0) {
-    a.out_seg_count[blockIdx.x] = s_cursor[0];
-    a.out_seg_count[G + blockIdx.x] = s_cursor[1];
-    const uint32_t total = s_cursor[0] + s_cursor[1];
+    uint32_t total = 0;
+    for (uint32_t c = 0; c < ncls; ++c) {
+      a.out_seg_count[c * G + blockIdx.x] = s_cursor[c];
+      total += s_cursor[c];
+    }
     if (total) atomicAdd(a.out_total, total);
     if (blockIdx.x == 0) *a.out_chunk = cap;
   }
@@ -2236,7 +2471,8 @@ int choose_mode(const DeviceScene& sc) {
 size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid, bool refill) {
   const size_t scene = (size_t)lds_scene_float4s(mode, node_float4s(sc.width), sc.num_nodes, sc.lds_nodes,
                                                  sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16;
-  const size_t scratch = ((size_t)2 * grid + 1 + 3) / 4 * 16;   // 2 segments per block + sentinel
+  // segment counts per block (2 classes; the lane-refill kernel reserves 4) + sentinel
+  const size_t scratch = ((size_t)(refill ? 4 : 2) * grid + 1 + 3) / 4 * 16;
   const size_t entry_words = sc.width == 8 ? 2 : 1;              // BVH8: two-word group entries
   const size_t lane_state = refill ? (size_t)kLaneStateWords * kBlock * 4 : 0;   // lane-refill kernel
   return scene + scratch + (size_t)stack * entry_words * kBlock * 4 + lane_state;   // stack = LDS entries (|STACK|)
@@ -2393,6 +2629,7 @@ hipError_t path_dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t st
 
 template <int STACK, int MODE, int WIDTH>
 hipError_t launch_bounce_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
+  if (a.classes != 2 && !use_refill<MODE, WIDTH>()) return hipErrorInvalidValue;   // 4 classes: lane-refill kernel only
   const DeviceScene f = fit_lds_nodes(sc, MODE, STACK < 0 ? -STACK : STACK, grid);
   const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, grid, use_refill<MODE, WIDTH>());
   if (use_refill<MODE, WIDTH>()) bounce_refill_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
@@ -2435,6 +2672,32 @@ hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_e
   if (stack_entries <= 16) return dispatch_width<16>(sc, a, grid, grid_out, s);
   if (stack_entries <= 24) return dispatch_width<24>(sc, a, grid, grid_out, s);
   return dispatch_width<32>(sc, a, grid, grid_out, s);
+}
+
+// chained wavefront: whole-scene-in-LDS scenes, BVH2/BVH4, the stack in LDS;
+// refuses a grid that is not resident at once (the kernel's waits need it)
+template <int STACK, int WIDTH>
+hipError_t launch_chain_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
+  const size_t lds = bounce_lds_bytes(sc, kAllLds, STACK, 0, false);
+  int dev = 0, occ = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return e;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, chain_kernel<STACK, kAllLds, WIDTH>, kBlock, lds);
+  if (e != hipSuccess) return e;
+  if ((uint64_t)std::min(occ, 8) * (uint64_t)prop.multiProcessorCount < grid) return hipErrorNotSupported;
+  chain_kernel<STACK, kAllLds, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(sc, a);
+  return hipGetLastError();
+}
+template <int STACK>
+hipError_t chain_width(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
+  return sc.width == 4 ? launch_chain_t<STACK, 4>(sc, a, grid, s) : launch_chain_t<STACK, 2>(sc, a, grid, s);
+}
+bool chain_ok(const DeviceScene& sc, uint32_t stack_entries) {
+  return (sc.width == 2 || sc.width == 4) && choose_mode(sc) == kAllLds && sc.max_stack <= stack_entries &&
+         stack_entries <= 32;
 }
 
 }  // namespace
@@ -2634,6 +2897,18 @@ hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* gr
 }
 
 bool path_preferred(const DeviceScene& sc) { return sc.width != 8 && choose_mode(sc) != kAllLds; }
+
+bool chain_supported(const DeviceScene& sc, uint32_t stack_entries) { return chain_ok(sc, stack_entries); }
+
+hipError_t launch_chain(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,
+                        hipStream_t s) {
+  if (!chain_ok(sc, stack_entries) || a.max_path_length > kChainMaxL) return hipErrorNotSupported;
+  if (stack_entries <= 8) return chain_width<8>(sc, a, grid, s);
+  if (stack_entries <= 12) return chain_width<12>(sc, a, grid, s);
+  if (stack_entries <= 16) return chain_width<16>(sc, a, grid, s);
+  if (stack_entries <= 24) return chain_width<24>(sc, a, grid, s);
+  return chain_width<32>(sc, a, grid, s);
+}
 
 }  // namespace MRT_NS
 }  // namespace mrt
