@@ -410,7 +410,7 @@ def main():
                      "counter": counter,
                      "limiter": "VALU issue + memory latency of BVH traversal (not HBM bandwidth)",
                      "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),
-                     "kernel": {1: "path_kernel (all bounces per launch)", 2: "chain_kernel (chained wavefront: all bounces per launch)"}.get(
+                     "kernel": {1: "path_kernel (all bounces per launch)", 2: "stream_kernel (wave-local streaming wavefront: all bounces per launch)"}.get(
                          st["kernel"], "bounce_kernel (one launch per bounce)"),
                      "launches": launches, "timed_launches": timed,
                      "avg_launch_ms": round(avg_launch_ms, 4),

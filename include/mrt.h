@@ -182,7 +182,7 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
   uint64_t owned_pixels;
   uint64_t timed_launches;         /* launches behind kernel_ms (every 8th frame's) */
   uint32_t kernel;                 /* the hot kernel: 0 = wavefront of per-bounce launches, 1 = path megakernel,
-                                      2 = chained wavefront (all bounces of a frame batch in one launch) */
+                                      2 = streaming wavefront (all bounces of a frame batch in one launch) */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);

@@ -51,26 +51,15 @@ constexpr uint32_t kSegSlack = 1024;
 constexpr uint32_t kRefillSlack = 2048;   // segment slack of the lane-refill kernel (kernels.hip)
 constexpr uint32_t kMaxSegSlack = kRefillSlack;
 
-// Chained wavefront (chain_kernel): every bounce of a batch in one launch;
-// block j publishes its bounce-b survivor segment into list j % kChainLists
-// of bounce b as soon as its four waves are done with bounce b, and waves
-// that have run out of bounce-b input take bounce-(b+1) rays from published
-// segments (kGrab at a time, per-segment grab counters).  Per batch, zeroed
-// before the launch: lists [L][kChainLists][ceil(G / kChainLists)] uint64
-// entries ((block + 1) | c0 << 16 | c1 << 40, 0 = not yet published), sync
-// words [L][kChainSyncWords] (list heads and fill counters 128 B apart, the
-// count of blocks that published), one error word, and the segment grab
-// counters [L][G][kChainGrabStride].
-constexpr uint32_t kChainLists = 16;
-constexpr uint32_t kChainSyncWords = 1152;
-constexpr uint32_t kChainHeadOff = 0, kChainFillOff = 512, kChainPubOff = 1024;
-constexpr uint32_t kChainGrabStride = 16;
-constexpr uint32_t kChainMaxCount = (1u << 24) - 1;   // c0, c1 field width
-inline size_t chain_list_len(uint32_t G) { return (G + kChainLists - 1) / kChainLists; }
-inline size_t chain_words(uint32_t L, uint32_t G) {   // uint32 words per batch
-  return (size_t)L * kChainLists * chain_list_len(G) * 2 + (size_t)L * kChainSyncWords + 32 +
-         (size_t)L * G * kChainGrabStride;
-}
+// Wave-local streaming wavefront (stream_kernel): every bounce of a batch in
+// one launch with no inter-wave hand-off.  Each wave keeps its own queue of
+// kStreamCap ray slots per bounce level 1..L-1 (SoA planes of RayQueue a.in_q,
+// level k of wave w at slots ((w * (L - 1)) + k - 1) * kStreamCap) and always
+// runs 64 rays of one bounce: the deepest level holding >= 64 rays, else 64
+// new camera rays; survivors go to the next level (< 2 * 64 rays each).
+constexpr uint32_t kStreamCap = 128;
+constexpr uint32_t kStreamMaxL = 64;
+inline size_t stream_slots(uint32_t L, uint32_t G) { return (size_t)G * 4 * (L > 1 ? L - 1 : 1) * kStreamCap; }
 
 struct BounceArgs {
   uint32_t width, height;
@@ -111,16 +100,7 @@ struct BounceArgs {
                                // owned pixel when its path ends (accumulated by launch_accumulate_frame)
   uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
                                // [grid * 256][max_stack (x2 for BVH8)] uint32 (null if none)
-  uint32_t* bounce_counts;     // path / chain kernel: [max_path_length] rays alive at the start of bounce b + 1
-  // chain kernel: the third survivor queue (bounce b reads ring[b % 3] and
-  // writes ring[(b + 1) % 3] of {in_q, out_q, ring2}) and the per-batch
-  // lists / sync words / grab counters (chain_words), error word set when a
-  // wait exceeded its bound (the launch then ends early with a wrong image)
-  RayQueue ring2;
-  uint64_t* chain_list;
-  uint32_t* chain_sync;
-  uint32_t* chain_grab;
-  uint32_t* chain_error;
+  uint32_t* bounce_counts;     // path / stream kernel: [max_path_length] rays alive at the start of bounce b + 1
 };
 
 // running-mean accumulation of one frame over the owned tiles
@@ -158,11 +138,11 @@ struct AccumArgs {
   hipError_t launch_paths(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,            \
                           uint32_t grid, hipStream_t s);                                                  \
   hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                   \
-  /* chained wavefront: all bounces of a batch in one launch over the bounce grid (whole-scene-in-LDS   \
-     BVH2/BVH4 scenes only; hipErrorNotSupported otherwise) */                                            \
-  hipError_t launch_chain(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,            \
-                          uint32_t grid, hipStream_t s);                                                  \
-  bool chain_supported(const DeviceScene& sc, uint32_t stack_entries);                                    \
+  /* wave-local streaming wavefront: all bounces of a batch in one launch, per-wave ray queues     \
+     (whole-scene-in-LDS BVH2/BVH4 scenes; hipErrorNotSupported otherwise) */                          \
+  hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
+                           uint32_t grid, hipStream_t s);                                                 \
+  bool stream_supported(const DeviceScene& sc, uint32_t stack_entries);                                   \
   /* the scene's LDS staging mode is not "whole scene in LDS": the path kernel is the faster one */      \
   bool path_preferred(const DeviceScene& sc);                                                             \
   /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \

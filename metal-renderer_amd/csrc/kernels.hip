@@ -1313,9 +1313,10 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n
 // output segment [out_base, out_base + cap) of `out_q` through the LDS
 // cursors (class 0 = left a diffuse surface, from the front; class 1 from
 // the back) and traces the shadow ray.  Returns the survivors written.
-// Used by bounce_kernel (one launch per bounce) and chain_kernel (all
-// bounces of a batch in one launch).
-template <int STACK, int MODE, int WIDTH>
+// Used by bounce_kernel (one launch per bounce) and, with WAVEQ (the wave's
+// own queue: survivors at out_base + their rank among the wave's survivors,
+// no cursors, no class split), by stream_kernel.
+template <int STACK, int MODE, int WIDTH, bool WAVEQ = false>
 __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const LdsCtx& cx, const BounceArgs& a,
                                                uint32_t bounce, bool active, uint32_t idx, uint32_t slot,
                                                const RayQueue& in_q, const RayQueue& out_q, uint32_t* cursor,
@@ -1403,12 +1404,12 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   // (mirror / plastic / dielectric: specular and refracted rays) from the
   // back; the next bounce reads all class-0 runs first, so its waves see
   // rays of one class (MRT_DEBUG bit 16: no partition)
-  const bool cls1 = (s.prevDiffuse == 0.0f) && !(a.debug & 16u);
+  const bool cls1 = !WAVEQ && (s.prevDiffuse == 0.0f) && !(a.debug & 16u);
   const uint64_t mask0 = __ballot(alive && !cls1), mask1 = __ballot(alive && cls1);
   uint32_t o = 0, wrote = 0;
   if (mask0 | mask1) {
     uint32_t w0 = 0, w1 = 0;
-    if (lane == 0) {
+    if (!WAVEQ && lane == 0) {
       if (mask0) w0 = atomicAdd(&cursor[0], (uint32_t)__popcll(mask0));
       if (mask1) w1 = atomicAdd(&cursor[1], (uint32_t)__popcll(mask1));
     }
@@ -1556,192 +1557,110 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
 
 
 // ---------------------------------------------------------------------------
-// Chained wavefront: every bounce of a frame batch in ONE launch over the
-// persistent bounce grid (whole-scene-in-LDS scenes, the C1/C2 class).
+// Wave-local streaming wavefront: every bounce of a frame batch in ONE launch
+// over the persistent bounce grid, with no hand-off between waves (the
+// whole-scene-in-LDS class: C1, C2).
 //
-// bounce_kernel ends each bounce at a launch boundary: the last grabs drain
-// at falling occupancy, the next launch stages the scene and scans the
-// segment counts again — about 60-110 us per launch, measured on one GPU's
-// 1/8 tile share of C2 (bounce launches of 0.35-1 ms).  Here a wave that
-// finds no bounce-b input left goes straight on to bounce b+1 and takes its
-// rays from the survivor segments of blocks that have already finished
-// bounce b, so the drain of bounce b overlaps bounce b+1 and only the last
-// bounce drains.
-//
-// Hand-off (cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md
-// "inter-workgroup visibility"): every wave of block j waits for its own
-// stores (s_waitcnt vmcnt(0)) before adding to the block's LDS done count;
-// the wave whose add is last releases at agent scope (L2 write-back) and then
-// publishes (j, c0, c1) with one relaxed agent-scope 8-B store into list
-// j % kChainLists of bounce b.  A consumer polls the entry relaxed, and before
-// its first load from a newly taken segment runs an agent-scope acquire.
-// Segments are taken kGrab rays at a time through per-segment grab counters;
-// the lists' heads only move past exhausted entries.
-//
-// Queues: a ring of three — bounce b reads ring[b % 3] and writes
-// ring[(b + 1) % 3], the queue bounce b - 2 read; a wave starts bounce b >= 2
-// only after every block has published bounce b - 2 (it has then finished
-// reading it).  Waiting is bounded (~2 s of s_memrealtime): on expiry the
-// wave sets chain_error and gives up (the host reports an error).  Every
-// block must be resident at once (the grid is the bounce grid: every resident
-// block slot, one launch at a time — frames in flight keep bounce_kernel).
+// bounce_kernel ends every bounce at a launch boundary: the last grabs drain
+// at falling occupancy and the next launch ramps up again — 60-110 us per
+// launch on one GPU's 1/8 tile share of C2 (launches of 0.35-1 ms), 1-3 % of
+// a whole-frame launch.  Here each wave keeps its own small queue per bounce
+// level (kStreamCap slots in HBM, written and re-read by the same CU, so
+// mostly L2 hits) and always runs a full wave of ONE bounce: the deepest
+// level holding >= 64 rays, else 64 new camera rays from the launch's grab
+// ranges.  Survivors go to the next level at the wave's own count (ballot +
+// popcount, no atomics).  Every iteration is a coherent 64-lane wave of one
+// bounce as in bounce_kernel (shading code path, noise table), the queues
+// never exceed 2 * 64 - 1 rays per level (a level is run as soon as it holds
+// 64 and deeper levels first), and only the end of the launch drains: once
+// the camera rays are gone a wave runs its partial levels, deepest first.
+// No wave ever waits for another, so any grid and any residency is safe.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kChainMaxL = 64;
-constexpr uint64_t kChainWaitTicks = 200000000ull;   // s_memrealtime is 100 MHz: 2 s
-
-__device__ __forceinline__ RayQueue ring_queue(const BounceArgs& a, uint32_t k) {
-  return k == 0 ? a.in_q : (k == 1 ? a.out_q : a.ring2);
-}
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int STACK, int MODE, int WIDTH>
-__global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void chain_kernel(DeviceScene sc, BounceArgs a) {
-  __shared__ uint32_t s_res[kChainMaxL], s_cur[kChainMaxL][2], s_done[kChainMaxL], s_lclosed[kChainMaxL];
+__global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(DeviceScene sc, BounceArgs a) {
+  __shared__ uint32_t s_cnt[kBlock / 64][kStreamMaxL];    // rays queued per level (wave-private rows)
+  __shared__ uint32_t s_alive[kBlock / 64][kStreamMaxL];  // survivors per bounce (stats)
   __shared__ uint32_t s_closed;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t G = gridDim.x, g = blockIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t L = a.max_path_length;
   const LdsCtx cx = stage_lds<MODE>(sc, 0, a.stack_spill);
-  for (uint32_t i = tid; i < L; i += kBlock) { s_res[i] = 0; s_cur[i][0] = s_cur[i][1] = 0; s_done[i] = 0; s_lclosed[i] = 0; }
+  for (uint32_t i = lane; i < L; i += 64u) { s_cnt[wave][i] = 0; s_alive[wave][i] = 0; }
   if (tid == 0) s_closed = 0;
   __syncthreads();
-
-  // one capacity for every bounce: survivors of any bounce <= N0
+  uint32_t* cnt = s_cnt[wave];
   const uint32_t N0 = a.num_slots * a.batch;
-  const uint32_t chunk = ((N0 + G - 1) / G + kBlock - 1) / kBlock * kBlock;
-  const uint32_t cap = chunk + kSegSlack;
-  const uint32_t out_base = g * cap;
   const uint32_t rlen = ((N0 + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
-  const uint32_t list_len = (G + kChainLists - 1) / kChainLists;
-  const uint32_t home = g % kChainLists;   // blocks j, j + 8 share an XCD: list g % 16 holds same-XCD segments
+  uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
   const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t cur_range = g % kGrabRanges, ranges_left = kGrabRanges;
-  uint32_t acq_seg = 0xFFFFFFFFu;   // the segment this wave last acquired
-  bool failed = false;               // a bounded wait expired (wave-uniform)
-
+  // this wave's queue: level k (1..L-1) at slots qbase + (k - 1) * kStreamCap
+  const uint32_t qbase = (blockIdx.x * (kBlock / 64u) + wave) * (L > 1 ? L - 1 : 1u) * kStreamCap;
+  uint32_t pend = 0, pend_end = 0;   // camera rays [pend, pend_end) of the wave's last grab not yet run
+  bool input = true;
   STAMP_DECL();   // stamp builds: phase cycles accumulate but are not flushed for this kernel
   const StampRef st = STAMP_REF();
-  for (uint32_t b = 0; b < L && !failed; ++b) {
-    const RayQueue in_q = ring_queue(a, b % 3u), out_q = ring_queue(a, (b + 1) % 3u);
-    // ring: bounce b writes the queue bounce b - 2 read
-    if (b >= 2) {
-      uint32_t ok = 1;
+  for (;;) {
+    // the deepest level holding a full wave (wave-uniform LDS reads)
+    uint32_t lvl = 0;
+    for (uint32_t k = L - 1; k >= 1; --k)
+      if (cnt[k] >= 64u) { lvl = k; break; }
+    if (lvl == 0 && input && pend >= pend_end) {
+      // grab kGrab camera rays from the launch's ranges (as bounce_kernel)
+      uint32_t got = 0xFFFFFFFFu, gend = 0;
       if (lane == 0) {
-        const uint32_t* pub = a.chain_sync + (size_t)(b - 2) * kChainSyncWords + kChainPubOff;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (ld_agent(pub) < G) {
-          if (__builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) { ok = 0; break; }
-          __builtin_amdgcn_s_sleep(4);
-        }
-      }
-      if (!__builtin_amdgcn_readfirstlane(ok)) { failed = true; break; }
-    }
-    const uint32_t* lsync = a.chain_sync + (size_t)(b ? b - 1 : 0) * kChainSyncWords;
-    const uint64_t* lists = a.chain_list + (size_t)(b ? b - 1 : 0) * kChainLists * list_len;
-    uint32_t* lheads = const_cast<uint32_t*>(lsync) + kChainHeadOff;
-    uint32_t cur_list = home;
-    for (;;) {
-      // reserve kGrab output slots of this block's bounce-b segment, then take
-      // up to kGrab rays: bounce 0 from the launch's grab ranges, later
-      // bounces from a published segment of bounce b - 1
-      uint32_t got = 0xFFFFFFFFu, gend = 0, sj = 0, sc0 = 0, sn = 0, werr = 0;
-      if (lane == 0) {
-        if (atomicAdd(&s_res[b], kGrab) + kGrab <= cap) {
-          if (b == 0) {
-            while (ranges_left) {
-              const uint32_t r0 = cur_range * rlen;
-              if (r0 < N0 && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
-                const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
-                if (i < rlen && r0 + i < N0) { got = r0 + i; gend = min(N0, r0 + rlen); break; }
-                atomicOr(&s_closed, 1u << cur_range);
-              }
-              cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
-              --ranges_left;
-            }
-          } else {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (;;) {
-              bool pending = false;
-              for (uint32_t t = 0; t < kChainLists && got == 0xFFFFFFFFu; ++t) {
-                const uint32_t r = cur_list;
-                const uint32_t size_r = G > r ? (G - r + kChainLists - 1) / kChainLists : 0u;
-                if (!(__hip_atomic_load(&s_lclosed[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << r))) {
-                  uint32_t pidx = ld_agent(lheads + r * 32u);
-                  for (;;) {
-                    if (pidx >= size_r) { atomicOr(&s_lclosed[b], 1u << r); break; }   // every entry exhausted
-                    const uint64_t e = ld_agent64(lists + (size_t)r * list_len + pidx);
-                    if (e == 0) { pending = true; break; }                                 // not yet published
-                    const uint32_t j = (uint32_t)(e & 0xFFFFu) - 1u;
-                    const uint32_t c0 = (uint32_t)(e >> 16) & kChainMaxCount, c1 = (uint32_t)(e >> 40);
-                    const uint32_t i = atomicAdd(a.chain_grab + ((size_t)(b - 1) * G + j) * kChainGrabStride, kGrab);
-                    if (i < c0 + c1) { got = i; gend = c0 + c1; sj = j; sc0 = c0; sn = c0 + c1; break; }
-                    atomicMax(lheads + r * 32u, pidx + 1u);
-                    ++pidx;
-                  }
-                }
-                if (got == 0xFFFFFFFFu) cur_list = cur_list + 1 == kChainLists ? 0u : cur_list + 1;
-              }
-              if (got != 0xFFFFFFFFu || !pending) break;
-              if (__builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) { werr = 1; break; }
-              __builtin_amdgcn_s_sleep(2);
-            }
+        while (ranges_left) {
+          const uint32_t r0 = cur_range * rlen;
+          if (r0 < N0 && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
+            const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
+            if (i < rlen && r0 + i < N0) { got = r0 + i; gend = min(N0, min(r0 + rlen, got + kGrab)); break; }
+            atomicOr(&s_closed, 1u << cur_range);
           }
-          if (got == 0xFFFFFFFFu) atomicSub(&s_res[b], kGrab);   // input exhausted
-        } else {
-          got = 0xFFFFFFFEu;   // the block's bounce-b output segment is full
+          cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
+          --ranges_left;
         }
       }
       got = __builtin_amdgcn_readfirstlane(got);
-      if (__builtin_amdgcn_readfirstlane(werr)) { failed = true; break; }
-      if (got >= 0xFFFFFFFEu) break;
-      gend = __builtin_amdgcn_readfirstlane(gend);
-      sj = __builtin_amdgcn_readfirstlane(sj);
-      sc0 = __builtin_amdgcn_readfirstlane(sc0);
-      sn = __builtin_amdgcn_readfirstlane(sn);
       cur_range = __builtin_amdgcn_readfirstlane(cur_range);
       ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
-      cur_list = __builtin_amdgcn_readfirstlane(cur_list);
-      if (b > 0 && sj != acq_seg) {   // first rays of a newly taken segment
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        acq_seg = sj;
+      if (got == 0xFFFFFFFFu) {
+        input = false;
+      } else {
+        pend = got;
+        pend_end = __builtin_amdgcn_readfirstlane(gend);
       }
-      const uint32_t gend_c = min(gend, got + kGrab);
-      uint32_t wrote = 0;
-      for (uint32_t it = 0; it < kGrab / 64u; ++it) {
-        const uint32_t off = got + it * 64u + lane;
-        const bool active = off < gend_c;
-        // segment sj: class 0 at [sj*cap, sj*cap + c0), class 1 at the end of its range
-        const uint32_t slot = off < sc0 ? sj * cap + off : sj * cap + cap - (sn - sc0) + (off - sc0);
-        wrote += bounce_wave<STACK, MODE, WIDTH>(sc, cx, a, b, active, off, slot, in_q, out_q, s_cur[b], out_base,
-                                                 cap, lanes_below, st);
-      }
-      if (lane == 0) atomicSub(&s_res[b], kGrab - wrote);
     }
-    if (failed || b + 1 == L) break;
-    // this wave is done with bounce b: its stores first, then the block's
-    // last wave releases and publishes the block's segment
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0 && atomicAdd(&s_done[b], 1u) == kBlock / 64u - 1u) {
-      const uint32_t c0 = s_cur[b][0], c1 = s_cur[b][1];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      uint32_t* sync = a.chain_sync + (size_t)b * kChainSyncWords;
-      const uint32_t r = g % kChainLists;
-      const uint32_t pos = atomicAdd(sync + kChainFillOff + r * 32u, 1u);
-      __hip_atomic_store(a.chain_list + ((size_t)b * kChainLists + r) * list_len + pos,
-                         (uint64_t)(g + 1u) | ((uint64_t)c0 << 16) | ((uint64_t)c1 << 40), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      atomicAdd(sync + kChainPubOff, 1u);
-      if (c0 + c1) atomicAdd(a.bounce_counts + b, c0 + c1);
+    uint32_t n, first;   // this iteration: n rays of level lvl
+    bool camera = false;
+    if (lvl == 0 && pend < pend_end) {
+      camera = true;
+      first = pend;
+      n = min(64u, pend_end - pend);
+      pend += n;
+    } else {
+      if (lvl == 0) {   // camera rays exhausted: the deepest non-empty level
+        for (uint32_t k = L - 1; k >= 1; --k)
+          if (cnt[k] > 0u) { lvl = k; break; }
+        if (lvl == 0) break;   // every level empty: the wave is done
+      }
+      n = min(64u, cnt[lvl]);
+      first = cnt[lvl] - n;   // run the top n, the rest stays in place
+      cnt[lvl] = first;
+    }
+    const bool active = lane < n;
+    const uint32_t idx = first + lane;                                  // camera: the launch's dense index
+    const uint32_t slot = qbase + (lvl - 1u) * kStreamCap + first + lane;   // level lvl >= 1: the queue slot
+    const uint32_t out = lvl + 1u < L ? qbase + lvl * kStreamCap + cnt[lvl + 1u] : 0u;
+    // the wave reads rays its own lanes wrote: their stores first
+    if (!camera) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t wrote = bounce_wave<STACK, MODE, WIDTH, true>(sc, cx, a, camera ? 0u : lvl, active, idx, slot,
+                                                                 a.in_q, a.in_q, nullptr, out, 0u, lanes_below, st);
+    if (lvl + 1u < L && lane == 0) {
+      cnt[lvl + 1u] += wrote;
+      s_alive[wave][lvl] += wrote;
     }
   }
-  if (failed && lane == 0) atomicOr(a.chain_error, 1u);
+  // stats: survivors of bounce b = rays alive at the start of bounce b + 1
+  for (uint32_t b = lane; b + 1 < L; b += 64u)
+    if (s_alive[wave][b]) atomicAdd(a.bounce_counts + b, s_alive[wave][b]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2674,28 +2593,18 @@ hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_e
   return dispatch_width<32>(sc, a, grid, grid_out, s);
 }
 
-// chained wavefront: whole-scene-in-LDS scenes, BVH2/BVH4, the stack in LDS;
-// refuses a grid that is not resident at once (the kernel's waits need it)
+// wave-local streaming wavefront: whole-scene-in-LDS scenes, BVH2/BVH4, the
+// stack in LDS
 template <int STACK, int WIDTH>
-hipError_t launch_chain_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
-  const size_t lds = bounce_lds_bytes(sc, kAllLds, STACK, 0, false);
-  int dev = 0, occ = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  hipDeviceProp_t prop;
-  e = hipGetDeviceProperties(&prop, dev);
-  if (e != hipSuccess) return e;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, chain_kernel<STACK, kAllLds, WIDTH>, kBlock, lds);
-  if (e != hipSuccess) return e;
-  if ((uint64_t)std::min(occ, 8) * (uint64_t)prop.multiProcessorCount < grid) return hipErrorNotSupported;
-  chain_kernel<STACK, kAllLds, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(sc, a);
+hipError_t launch_stream_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
+  stream_kernel<STACK, kAllLds, WIDTH><<<dim3(grid), dim3(kBlock), bounce_lds_bytes(sc, kAllLds, STACK, 0, false), s>>>(sc, a);
   return hipGetLastError();
 }
 template <int STACK>
-hipError_t chain_width(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
-  return sc.width == 4 ? launch_chain_t<STACK, 4>(sc, a, grid, s) : launch_chain_t<STACK, 2>(sc, a, grid, s);
+hipError_t stream_width(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
+  return sc.width == 4 ? launch_stream_t<STACK, 4>(sc, a, grid, s) : launch_stream_t<STACK, 2>(sc, a, grid, s);
 }
-bool chain_ok(const DeviceScene& sc, uint32_t stack_entries) {
+bool stream_ok(const DeviceScene& sc, uint32_t stack_entries) {
   return (sc.width == 2 || sc.width == 4) && choose_mode(sc) == kAllLds && sc.max_stack <= stack_entries &&
          stack_entries <= 32;
 }
@@ -2898,16 +2807,16 @@ hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* gr
 
 bool path_preferred(const DeviceScene& sc) { return sc.width != 8 && choose_mode(sc) != kAllLds; }
 
-bool chain_supported(const DeviceScene& sc, uint32_t stack_entries) { return chain_ok(sc, stack_entries); }
+bool stream_supported(const DeviceScene& sc, uint32_t stack_entries) { return stream_ok(sc, stack_entries); }
 
-hipError_t launch_chain(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,
-                        hipStream_t s) {
-  if (!chain_ok(sc, stack_entries) || a.max_path_length > kChainMaxL) return hipErrorNotSupported;
-  if (stack_entries <= 8) return chain_width<8>(sc, a, grid, s);
-  if (stack_entries <= 12) return chain_width<12>(sc, a, grid, s);
-  if (stack_entries <= 16) return chain_width<16>(sc, a, grid, s);
-  if (stack_entries <= 24) return chain_width<24>(sc, a, grid, s);
-  return chain_width<32>(sc, a, grid, s);
+hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,
+                         hipStream_t s) {
+  if (!stream_ok(sc, stack_entries) || a.max_path_length > kStreamMaxL) return hipErrorNotSupported;
+  if (stack_entries <= 8) return stream_width<8>(sc, a, grid, s);
+  if (stack_entries <= 12) return stream_width<12>(sc, a, grid, s);
+  if (stack_entries <= 16) return stream_width<16>(sc, a, grid, s);
+  if (stack_entries <= 24) return stream_width<24>(sc, a, grid, s);
+  return stream_width<32>(sc, a, grid, s);
 }
 
 }  // namespace MRT_NS

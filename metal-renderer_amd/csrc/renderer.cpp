@@ -124,7 +124,7 @@ constexpr int kDrawRing = 3;
 struct FrameSlot {
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  DevBuf queue[3][4];       // ray queues (the chained wavefront uses a ring of three)
+  DevBuf queue[2][4];       // ray queues (the streaming wavefront: queue[0] holds the per-wave queues)
   DevBuf segments;          // 2 x grid per-block survivor counts + 2 chunk words
   DevBuf radiance;          // W*H float4, written once per owned pixel per frame
   DevBuf spill;             // traversal stack entries beyond the LDS capacity (deep BVHs)
@@ -183,9 +183,8 @@ struct mrt_renderer {
   uint32_t batch = 1;           // frames per bounce launch (frame batching)
   mrt_stats stats{};
   uint32_t stack_entries = 32;
-  bool chain_allowed = false;   // chained wavefront possible for this scene / configuration
-  bool chain_mode = false;  // wavefront as one chained launch per frame batch (chain_kernel)
-  DevBuf chain;             // per-batch lists / sync words / grab counters of the chained launches
+  bool stream_allowed = false;  // streaming wavefront possible for this scene / configuration
+  bool stream_mode = false; // wavefront as one launch per frame batch with per-wave queues (stream_kernel)
   bool path_mode = true;   // one path-megakernel launch per frame batch (else L bounce launches, MRT_KERNEL=wave)
   bool use_qbvh = true;    // path kernel on the quantised BVH4 when the scene has one (MRT_QBVH=1 scenes)
   const mrt::DeviceScene& path_scene() const {
@@ -205,12 +204,8 @@ int finalize_draw(mrt_renderer* r, DrawRecord& d) {
   float ms = 0.0f;
   HIP_TRY(hipEventElapsedTime(&ms, d.start, d.stop));
   const uint32_t L = r->desc.max_path_length;
-  std::vector<uint32_t> cnt((size_t)d.launches * L + 1);   // + the chained launches' error word
+  std::vector<uint32_t> cnt((size_t)d.launches * L);
   HIP_TRY(hipMemcpy(cnt.data(), d.counters.p, cnt.size() * 4, hipMemcpyDeviceToHost));
-  if (cnt.back()) {
-    d.pending = false;
-    return fail(MRT_ERR_HIP, "chained bounce launch: a bounded wait expired (blocks not co-resident?)");
-  }
   uint64_t active = r->owned_pixels * d.frames;   // bounce 0: every owned pixel's camera ray
   for (uint32_t k = 0; k < d.launches; ++k)
     for (uint32_t b = 0; b + 1 < L; ++b) active += cnt[(size_t)k * L + b];
@@ -218,7 +213,7 @@ int finalize_draw(mrt_renderer* r, DrawRecord& d) {
   r->stats.last_draw_ms = ms;
   const uint64_t paths = r->owned_pixels * d.frames;
   r->stats.mpaths_per_s = ms > 0.0f ? (double)paths / (ms * 1e-3) / 1e6 : 0.0;
-  r->stats.kernel_launches += (uint64_t)d.launches * (r->path_mode || r->chain_mode ? 1u : L);
+  r->stats.kernel_launches += (uint64_t)d.launches * (r->path_mode || r->stream_mode ? 1u : L);
   if (r->desc.flags & MRT_FLAG_PROFILE) {
     for (size_t k = 0; k + 1 < d.events; k += 2) {
       float ms_k = 0.0f;
@@ -298,15 +293,16 @@ int alloc_frame_buffers(mrt_renderer* r) {
   // queue capacity: every owned slot of the batch + per-block rounding and
   // slack of the segments (kernels.h)
   const size_t slots = owned_slots * r->batch + (size_t)r->grid * (256 + mrt::kMaxSegSlack);
-  // chained launches pack a segment's class counts into 24-bit fields
-  r->chain_mode = r->chain_allowed &&
-                  (owned_slots * r->batch + r->grid - 1) / r->grid + 256 + mrt::kSegSlack <= mrt::kChainMaxCount;
+  r->stream_mode = r->stream_allowed;
   for (FrameSlot& fs : r->slots) {
     HIP_TRY(fs.segments.alloc(((size_t)8 * r->grid + 2) * 4));   // 2 queues x 4 classes x grid + 2 chunk words
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
-    for (int q = 0; q < 3; ++q)   // the path kernel keeps the path state in LDS: no ray queues
+    // the path kernel keeps the path state in LDS: no ray queues; the
+    // streaming wavefront needs only its per-wave queues
+    const size_t qslots = r->stream_mode ? mrt::stream_slots(r->desc.max_path_length, r->grid) : slots * (r->classes / 2);
+    for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 4; ++p)
-        HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (q == 2 && !r->chain_mode) ? 0 : slots * (r->classes / 2) * 16));
+        HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (r->stream_mode && q == 1) ? 0 : qslots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
     // spill rows of max_stack words per lane (BVH8 group entries: two words;
@@ -323,7 +319,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
   r->frame_index = 0;
   r->stats = mrt_stats{};
   r->stats.owned_pixels = r->owned_pixels;
-  r->stats.kernel = r->path_mode ? 1u : (r->chain_mode ? 2u : 0u);
+  r->stats.kernel = r->path_mode ? 1u : (r->stream_mode ? 2u : 0u);
   return MRT_OK;
 }
 
@@ -332,9 +328,9 @@ inline hipError_t launch_bounce(const mrt_renderer* r, const mrt::BounceArgs& a,
   return mrt::fast::launch_bounce(r->scene->dev, a, r->stack_entries, r->grid, s);
 }
 
-inline hipError_t launch_chain(const mrt_renderer* r, const mrt::BounceArgs& a, hipStream_t s) {
-  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_chain(r->scene->dev, a, r->stack_entries, r->grid, s);
-  return mrt::fast::launch_chain(r->scene->dev, a, r->stack_entries, r->grid, s);
+inline hipError_t launch_stream(const mrt_renderer* r, const mrt::BounceArgs& a, hipStream_t s) {
+  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_stream(r->scene->dev, a, r->stack_entries, r->grid, s);
+  return mrt::fast::launch_stream(r->scene->dev, a, r->stack_entries, r->grid, s);
 }
 
 inline hipError_t launch_paths(const mrt_renderer* r, const mrt::BounceArgs& a, hipStream_t s) {
@@ -1157,14 +1153,13 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid)
                                              : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid));
   if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
-  // chained wavefront (one launch per frame batch instead of one per bounce)
-  // for whole-scene-in-LDS scenes; it needs every block resident at once, so
-  // not with frames in flight or a forced grid; MRT_CHAIN=0 keeps bounce_kernel
+  // streaming wavefront (one launch per frame batch, per-wave ray queues)
+  // for whole-scene-in-LDS scenes; MRT_STREAM=0 keeps one launch per bounce
   {
-    const char* c = std::getenv("MRT_CHAIN");
+    const char* c = std::getenv("MRT_STREAM");
     const bool want = !c || std::atoi(c) != 0;
-    r->chain_allowed = want && !r->path_mode && r->inflight == 1 && !std::getenv("MRT_GRID") &&
-                    desc->max_path_length <= 64 && mrt::fast::chain_supported(desc->scene->dev, r->stack_entries);
+    r->stream_allowed = want && !r->path_mode && desc->max_path_length <= mrt::kStreamMaxL &&
+                        mrt::fast::stream_supported(desc->scene->dev, r->stack_entries);
   }
   // four-way material re-sort (one class per BSDF) for the lane-refill
   // wavefront of global-memory scenes; measured, not the default
@@ -1215,18 +1210,13 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   const uint32_t L = r->desc.max_path_length;
   const uint32_t B = r->batch;
   const uint32_t nb = (n + B - 1) / B;   // launches of up to B frames each
-  const size_t counter_bytes = ((size_t)nb * L + 1) * 4;   // + the chained launches' error word
+  const size_t counter_bytes = (size_t)nb * L * 4;
   if (d.counters.bytes < counter_bytes) HIP_TRY(d.counters.alloc(counter_bytes));
   HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, r->stream));
   const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
   if (r->grabs.bytes < (size_t)nb * L * grab_words * 4) HIP_TRY(r->grabs.alloc((size_t)nb * L * grab_words * 4));
   HIP_TRY(hipMemsetAsync(r->grabs.p, 0, (size_t)nb * L * grab_words * 4, r->stream));
-  const uint32_t launches_per_batch = r->path_mode || r->chain_mode ? 1u : L;
-  const size_t chain_words = r->chain_mode ? mrt::chain_words(L, r->grid) : 0;
-  if (r->chain_mode) {
-    if (r->chain.bytes < (size_t)nb * chain_words * 4) HIP_TRY(r->chain.alloc((size_t)nb * chain_words * 4));
-    HIP_TRY(hipMemsetAsync(r->chain.p, 0, (size_t)nb * chain_words * 4, r->stream));
-  }
+  const uint32_t launches_per_batch = r->path_mode || r->stream_mode ? 1u : L;
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
     const size_t need = (size_t)2 * ((nb + r->profile_every - 1) / r->profile_every) * launches_per_batch;
@@ -1277,23 +1267,10 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.radiance = fs.radiance.as<float4>();
       a.stack_spill = fs.spill.as<uint32_t>();
       a.bounce_counts = cnt + (size_t)k * L;
-      if (r->chain_mode) {   // one launch: bounce b reads queue b % 3, writes (b + 1) % 3
-        for (int p = 0; p < 4; ++p) {
-          a.in_q.plane[p] = fs.queue[0][p].as<float4>();
-          a.out_q.plane[p] = fs.queue[1][p].as<float4>();
-          a.ring2.plane[p] = fs.queue[2][p].as<float4>();
-        }
-        uint32_t* cw = r->chain.as<uint32_t>() + (size_t)k * chain_words;
-        const size_t list_words = (size_t)L * mrt::kChainLists * mrt::chain_list_len(r->grid) * 2;
-        a.chain_list = reinterpret_cast<uint64_t*>(cw);
-        a.chain_sync = cw + list_words;
-        a.chain_grab = cw + list_words + (size_t)L * mrt::kChainSyncWords + 32;
-        a.chain_error = cnt + (size_t)nb * L;
-      }
       const bool timed = profile && (k % r->profile_every) == 0;
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
       if (r->path_mode) HIP_TRY(launch_paths(r, a, fs.stream));
-      else if (r->chain_mode) HIP_TRY(launch_chain(r, a, fs.stream));
+      else if (r->stream_mode) HIP_TRY(launch_stream(r, a, fs.stream));
       else HIP_TRY(launch_bounce(r, a, fs.stream));
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
     }

@@ -1,11 +1,11 @@
-"""GPU: the chained wavefront (kernels.hip::chain_kernel) — every bounce of a
-frame batch in one launch, bounce b+1 taking its rays from the survivor
-segments blocks publish while other blocks still run bounce b — renders
-exactly what one launch per bounce (bounce_kernel, MRT_CHAIN=0) renders.
+"""GPU: the wave-local streaming wavefront (kernels.hip::stream_kernel) —
+every bounce of a frame batch in one launch, each wave running 64 rays of one
+bounce at a time from its own per-level queues — renders exactly what one
+launch per bounce (bounce_kernel, MRT_STREAM=0) renders.
 
-Rays carry their pixel slot, so the order in which segments are consumed
-never changes a path: images and active-ray counts must be bitwise equal, in
-both builds, for every path length, ragged frame, tile shard and batch size
+Rays carry their pixel slot, so the order in which a wave runs them never
+changes a path: images and active-ray counts must be bitwise equal, in both
+builds, for every path length, ragged frame, tile shard and batch size
 (renderer/Renderer.mm:500-585 is the per-bounce loop both restate)."""
 import numpy as np
 import pytest
@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _render(mrt_mod, monkeypatch, scene, W, H, L, frames, chain, precise, shard=(0, 1), batch=None, draws=1):
-    monkeypatch.setenv("MRT_CHAIN", "1" if chain else "0")
+    monkeypatch.setenv("MRT_STREAM", "1" if chain else "0")
     if batch:
         monkeypatch.setenv("MRT_BATCH", str(batch))
     else:
@@ -35,7 +35,7 @@ def boxes(mrt_mod):
 @pytest.mark.parametrize("precise", [True, False])
 @pytest.mark.parametrize("scene,W,H,L", [("cornellbox", 64, 48, 4), ("cornellbox", 333, 97, 7),
                                          ("white-box", 200, 120, 2), ("cornellbox", 96, 64, 1)])
-def test_chain_equals_per_bounce_launches(gpu, mrt_mod, monkeypatch, boxes, precise, scene, W, H, L):
+def test_stream_equals_per_bounce_launches(gpu, mrt_mod, monkeypatch, boxes, precise, scene, W, H, L):
     a, sa = _render(mrt_mod, monkeypatch, boxes[scene], W, H, L, 3, True, precise)
     b, sb = _render(mrt_mod, monkeypatch, boxes[scene], W, H, L, 3, False, precise)
     assert sa["kernel"] == 2 and sb["kernel"] == 0
@@ -46,27 +46,28 @@ def test_chain_equals_per_bounce_launches(gpu, mrt_mod, monkeypatch, boxes, prec
 
 
 @pytest.mark.parametrize("shard", [(0, 3), (2, 3), (5, 8)])
-def test_chain_tile_shards(gpu, mrt_mod, monkeypatch, boxes, shard):
-    """Small shares are what the chained launch is for (one GPU's 1/8 of a
+def test_stream_tile_shards(gpu, mrt_mod, monkeypatch, boxes, shard):
+    """Small shares are what the single launch is for (one GPU's 1/8 of a
     frame): each rank's tiles render bitwise as with per-bounce launches."""
     a, sa = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 520, 300, 4, 4, True, True, shard=shard)
     b, sb = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 520, 300, 4, 4, False, True, shard=shard)
     assert a.tobytes() == b.tobytes() and sa["active_ray_bounces"] == sb["active_ray_bounces"]
 
 
-def test_chain_batches_and_draws(gpu, mrt_mod, monkeypatch, boxes):
-    """Several batches per draw (one chained launch each, fresh lists and
-    counters per batch) and consecutive draws: bitwise as per-bounce."""
+def test_stream_batches_and_draws(gpu, mrt_mod, monkeypatch, boxes):
+    """Several batches per draw (one launch each, the per-wave queues reused)
+    and consecutive draws: bitwise as per-bounce."""
     a, sa = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 160, 96, 5, 7, True, False, batch=3, draws=2)
     b, sb = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 160, 96, 5, 7, False, False, batch=3, draws=2)
     assert sa["kernel_launches"] == 2 * 3 and sb["kernel_launches"] == 2 * 3 * 5
     assert a.tobytes() == b.tobytes() and sa["active_ray_bounces"] == sb["active_ray_bounces"]
 
 
-def test_chain_not_used_with_frames_in_flight(gpu, mrt_mod, monkeypatch, boxes):
-    """Two chained launches resident together could wait on each other's
-    blocks: with frames in flight the renderer keeps per-bounce launches."""
-    monkeypatch.setenv("MRT_INFLIGHT", "2")
-    r = mrt_mod.Renderer(boxes["cornellbox"], 64, 48, 4)
-    assert r.stats()["kernel"] == 0
-    r.close()
+def test_stream_with_frames_in_flight(gpu, mrt_mod, monkeypatch, boxes):
+    """Waves never wait for each other, so launches of different frame
+    batches may share the GPU: frames in flight stay bitwise."""
+    a, sa = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 200, 120, 4, 7, True, False, batch=2, draws=2)
+    monkeypatch.setenv("MRT_INFLIGHT", "3")
+    b, sb = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 200, 120, 4, 7, True, False, batch=2, draws=2)
+    assert sa["kernel"] == 2 and sb["kernel"] == 2
+    assert a.tobytes() == b.tobytes() and sa["active_ray_bounces"] == sb["active_ray_bounces"]
