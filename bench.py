@@ -3,7 +3,7 @@
 
 Metric (BASELINE.json): Mpaths/s at 1920x1080, 4 bounces (config C2:
 cornellbox, 64 spp, L = 4, diffuse).  One "step" = one complete C2 render:
-reset + 64 frames (1 spp each, L bounce launches per frame) on the tiles this
+reset + 64 frames (1 spp each; one launch of the hot kernel per 64-frame batch) on the tiles this
 rank owns, plus — for N > 1 — the single RCCL exchange of the accumulation
 image to rank 0, done by libmrt itself (mrt_renderer_exchange: a gather of
 the packed owned tiles, overlapped with the next step's draw; or an in-place

@@ -23,7 +23,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-HOT = ("bounce_", "path_kernel")   # the hot kernel: wavefront bounce kernels or the path megakernel
+HOT = ("bounce_", "path_kernel", "stream_kernel")   # the hot kernel: wavefront kernels or the path megakernel
 
 
 def counters(path):
@@ -84,7 +84,7 @@ def main(tag="r1", cfg="c2"):
                  f"{valu_frac if valu_frac is None else round(valu_frac, 3)}")
     md5_path = os.path.join(src, "lib.md5")
     lib_md5 = open(md5_path).read().strip() if os.path.exists(md5_path) else None
-    m = re.search(r"(bounce_\w*kernel|path_kernel)<[^>]*>", bounce["Name"])
+    m = re.search(r"(bounce_\w*kernel|path_kernel|stream_kernel)<[^>]*>", bounce["Name"])
     kernel = m.group(0) if m else bounce["Name"][:60]
     lines.append(f"* measured library: lib/libmrt.so md5 {lib_md5}, repository commit {commit}")
     with open(os.path.join(out, f"{tag}_{cfg}_summary.md"), "w") as f:

@@ -13,7 +13,7 @@ BENCH="python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline $*"
 set -o pipefail
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1; local rc=$?; tail -n 3 $OUT/$name.log; echo "== $name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -f csv -- $BENCH
-step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'bounce_|path_kernel' -d $OUT/fetch -o run -f csv -- $BENCH
-step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'bounce_|path_kernel' -d $OUT/write -o run -f csv -- $BENCH
-step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex 'bounce_|path_kernel' -d $OUT/sq -o run -f csv -- $BENCH
-step clk 400 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex 'bounce_|path_kernel' -d $OUT/clk -o run -f csv -- $BENCH
+step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/fetch -o run -f csv -- $BENCH
+step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/write -o run -f csv -- $BENCH
+step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/sq -o run -f csv -- $BENCH
+step clk 400 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/clk -o run -f csv -- $BENCH
