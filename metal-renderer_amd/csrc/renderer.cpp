@@ -129,16 +129,6 @@ struct FrameSlot {
   DevBuf radiance;          // W*H float4, written once per owned pixel per frame
   DevBuf spill;             // traversal stack entries beyond the LDS capacity (deep BVHs)
   hipEvent_t acc_done = nullptr;
-  // one slot (no frames in flight): the hot kernels run on their own stream
-  // `kstream` and write radiance[i] (two buffers, alternating per batch);
-  // the accumulate pass of a batch runs on the renderer's stream behind
-  // kdone[i], so the next batch's kernel (the next draw's too) starts while
-  // the previous batch is accumulated.  The kernel stream waits accd[i]
-  // before overwriting radiance[i].
-  hipStream_t kstream = nullptr;
-  DevBuf radiance2;
-  hipEvent_t kdone[2] = {nullptr, nullptr}, accd[2] = {nullptr, nullptr};
-  bool accd_rec[2] = {false, false};
 };
 
 // RCCL communicator of one rank (one process per GPU) and the stream its
@@ -201,8 +191,6 @@ struct mrt_renderer {
     return use_qbvh && scene->qdev.width == 5 ? scene->qdev : scene->dev;
   }
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
-  bool overlap = false;   // kernels on slot 0's kstream, accumulates on `stream` (FrameSlot)
-  uint32_t rad_seq = 0;   // radiance buffer of the next batch (overlap)
   uint32_t classes = 2;  // material classes of the survivor partition (MRT_CLASSES=4: lane-refill kernel only)
   Exchange x;
   DevBuf reference, display;   // comparison image (mrt_renderer_load_reference) and blit output
@@ -316,8 +304,6 @@ int alloc_frame_buffers(mrt_renderer* r) {
       for (int p = 0; p < 4; ++p)
         HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (r->stream_mode && q == 1) ? 0 : qslots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
-    if (fs.kstream) HIP_TRY(fs.radiance2.alloc(owned_slots * r->batch * 16));
-    fs.accd_rec[0] = fs.accd_rec[1] = false;
     const uint32_t need = r->scene->dev.max_stack;
     // spill rows of max_stack words per lane (BVH8 group entries: two words;
     // kernels.hip LdsCtx::spill_lane)
@@ -330,8 +316,6 @@ int alloc_frame_buffers(mrt_renderer* r) {
     HIP_TRY(hipMalloc(&r->image, (size_t)W * H * 16));
   }
   HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)W * H * 16, r->stream));
-  // the kernel stream (overlap) reads buffers memset on `stream` above
-  if (r->overlap) HIP_TRY(hipStreamSynchronize(r->stream));
   r->frame_index = 0;
   r->stats = mrt_stats{};
   r->stats.owned_pixels = r->owned_pixels;
@@ -1152,20 +1136,6 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     }
     HIP_TRY(hipEventCreateWithFlags(&fs.acc_done, hipEventDisableTiming));
   }
-  // one slot: overlap each batch's accumulate pass with the next kernel
-  // (MRT_OVERLAP=0: kernels and accumulates in one stream)
-  {
-    const char* v = std::getenv("MRT_OVERLAP");
-    r->overlap = r->inflight == 1 && (!v || std::atoi(v) != 0);
-    if (r->overlap) {
-      FrameSlot& fs = r->slots[0];
-      HIP_TRY(hipStreamCreateWithFlags(&fs.kstream, hipStreamNonBlocking));
-      for (int i = 0; i < 2; ++i) {
-        HIP_TRY(hipEventCreateWithFlags(&fs.kdone[i], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&fs.accd[i], hipEventDisableTiming));
-      }
-    }
-  }
   // kernel: scenes traversed from global memory run the path megakernel (all
   // bounces of a frame batch in one launch: C3 +15 %, C4 +1.5 % over the
   // wavefront), scenes staged whole in LDS the wavefront of per-bounce
@@ -1240,15 +1210,12 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   const uint32_t L = r->desc.max_path_length;
   const uint32_t B = r->batch;
   const uint32_t nb = (n + B - 1) / B;   // launches of up to B frames each
-  // the stream the hot kernels run on (overlap: slot 0's kernel stream; the
-  // counters and grab counters are only touched by those kernels)
-  hipStream_t ks = r->overlap ? r->slots[0].kstream : r->stream;
   const size_t counter_bytes = (size_t)nb * L * 4;
   if (d.counters.bytes < counter_bytes) HIP_TRY(d.counters.alloc(counter_bytes));
-  HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, ks));
+  HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, r->stream));
   const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
   if (r->grabs.bytes < (size_t)nb * L * grab_words * 4) HIP_TRY(r->grabs.alloc((size_t)nb * L * grab_words * 4));
-  HIP_TRY(hipMemsetAsync(r->grabs.p, 0, (size_t)nb * L * grab_words * 4, ks));
+  HIP_TRY(hipMemsetAsync(r->grabs.p, 0, (size_t)nb * L * grab_words * 4, r->stream));
   const uint32_t launches_per_batch = r->path_mode || r->stream_mode ? 1u : L;
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
@@ -1259,7 +1226,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       d.kernel_events.push_back(e);
     }
   }
-  HIP_TRY(hipEventRecord(d.start, ks));
+  HIP_TRY(hipEventRecord(d.start, r->stream));
   for (uint32_t k = 1; k < r->inflight; ++k) HIP_TRY(hipStreamWaitEvent(r->slots[k].stream, d.start, 0));
   uint32_t* cnt = d.counters.as<uint32_t>();
   size_t ev = 0;
@@ -1268,10 +1235,6 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     const uint64_t f = r->frame_index + (uint64_t)k * B;
     const uint32_t batch = std::min<uint32_t>(B, n - k * B);
     FrameSlot& fs = r->slots[k % r->inflight];
-    const hipStream_t kst = r->overlap ? fs.kstream : fs.stream;
-    const uint32_t ri = r->overlap ? (r->rad_seq++ & 1u) : 0u;   // radiance buffer of this batch
-    float4* const rad = (ri ? fs.radiance2 : fs.radiance).as<float4>();
-    if (r->overlap && fs.accd_rec[ri]) HIP_TRY(hipStreamWaitEvent(kst, fs.accd[ri], 0));   // its last reader
     uint32_t* seg = fs.segments.as<uint32_t>();
     uint32_t* meta = seg + 8 * (size_t)r->grid;
     for (uint32_t b = 0; b < launches_per_batch; ++b) {
@@ -1301,19 +1264,15 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       }
       a.noise_window = r->noise_window.as<float4>();
       a.noise_offset = (uint32_t)((int64_t)f - r->noise_first);
-      a.radiance = rad;
+      a.radiance = fs.radiance.as<float4>();
       a.stack_spill = fs.spill.as<uint32_t>();
       a.bounce_counts = cnt + (size_t)k * L;
       const bool timed = profile && (k % r->profile_every) == 0;
-      if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], kst));
-      if (r->path_mode) HIP_TRY(launch_paths(r, a, kst));
-      else if (r->stream_mode) HIP_TRY(launch_stream(r, a, kst));
-      else HIP_TRY(launch_bounce(r, a, kst));
-      if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], kst));
-    }
-    if (r->overlap) {   // the accumulate pass on the renderer's stream, behind this batch's kernels
-      HIP_TRY(hipEventRecord(fs.kdone[ri], kst));
-      HIP_TRY(hipStreamWaitEvent(fs.stream, fs.kdone[ri], 0));
+      if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
+      if (r->path_mode) HIP_TRY(launch_paths(r, a, fs.stream));
+      else if (r->stream_mode) HIP_TRY(launch_stream(r, a, fs.stream));
+      else HIP_TRY(launch_bounce(r, a, fs.stream));
+      if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
     }
     // accumulateImage for frames f .. f+batch-1, after the previous batch's
     // (running mean order)
@@ -1327,14 +1286,10 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     acc.shard_count = r->desc.shard_count;
     acc.tiles_x = r->tiles_x;
     acc.num_slots = r->owned_tiles * 4096u;
-    acc.radiance = rad;
+    acc.radiance = fs.radiance.as<float4>();
     acc.image = reinterpret_cast<float4*>(r->image);
     HIP_TRY(launch_accumulate_frame(r, acc, fs.stream));
     HIP_TRY(hipEventRecord(fs.acc_done, fs.stream));
-    if (r->overlap) {
-      HIP_TRY(hipEventRecord(fs.accd[ri], fs.stream));
-      fs.accd_rec[ri] = true;
-    }
     prev = &fs;
   }
   // join every slot back into the main stream
@@ -1467,13 +1422,7 @@ int mrt_renderer_destroy(mrt_renderer* r) {
   }
   if (r->own_image && r->image) (void)hipFree(r->image);
   for (FrameSlot& fs : r->slots) {
-    if (fs.kstream) (void)hipStreamSynchronize(fs.kstream);
     if (fs.acc_done) (void)hipEventDestroy(fs.acc_done);
-    for (int i = 0; i < 2; ++i) {
-      if (fs.kdone[i]) (void)hipEventDestroy(fs.kdone[i]);
-      if (fs.accd[i]) (void)hipEventDestroy(fs.accd[i]);
-    }
-    if (fs.kstream) (void)hipStreamDestroy(fs.kstream);
     if (fs.own_stream) (void)hipStreamDestroy(fs.stream);
   }
   r->slots.clear();

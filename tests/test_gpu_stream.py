@@ -71,28 +71,3 @@ def test_stream_with_frames_in_flight(gpu, mrt_mod, monkeypatch, boxes):
     b, sb = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 200, 120, 4, 7, True, False, batch=2, draws=2)
     assert sa["kernel"] == 2 and sb["kernel"] == 2
     assert a.tobytes() == b.tobytes() and sa["active_ray_bounces"] == sb["active_ray_bounces"]
-
-
-@pytest.mark.parametrize("scene,L", [("cornellbox", 4), ("CornellBox-Water-plastic", 8)])
-def test_accumulate_overlap_bitwise(gpu, mrt_mod, monkeypatch, scene, L):
-    """MRT_OVERLAP (default with one slot): kernels on their own stream into
-    two alternating radiance buffers, each batch's accumulate pass on the
-    renderer's stream behind it — so a batch's kernel runs while the previous
-    batch accumulates.  Several batches, draws and a reset in between must
-    equal the single-stream order bitwise (the running mean is order-dependent)."""
-    sc = mrt_mod.Scene(scene)
-    out = {}
-    for ov in ("0", "1"):
-        monkeypatch.setenv("MRT_OVERLAP", ov)
-        monkeypatch.setenv("MRT_BATCH", "2")
-        r = mrt_mod.Renderer(sc, 160, 96, L)
-        r.draw(5)
-        r.draw(3)
-        mid = r.read_image()
-        r.reset()
-        r.draw(4)
-        out[ov] = (mid, r.read_image(), r.stats()["active_ray_bounces"])
-        r.close()
-    assert np.isfinite(out["1"][1]).all() and out["1"][1][..., :3].max() > 0
-    assert out["0"][0].tobytes() == out["1"][0].tobytes()
-    assert out["0"][1].tobytes() == out["1"][1].tobytes() and out["0"][2] == out["1"][2]
