@@ -162,6 +162,88 @@ struct Builder {
     return id;
   }
 
+  // ---- full sweep SAH (opt.full_sweep): every node takes the exact best
+  // split over its centroid-sorted triangles on all three axes.  The node's
+  // triangles are kept sorted per axis in srt[0..2] over the same range
+  // [first, first + count) (one initial sort, ties by index); a split on axis
+  // a at k keeps srt[a] as is and stably partitions the other two by side, so
+  // the whole build is O(n log n) after the sort.  Leaves read srt[0]
+  // (copied to `order` at the end).
+  std::vector<uint32_t> srt[3], tmp;
+  std::vector<uint8_t> side;
+  std::vector<float> racc;
+
+  void init_full(uint32_t n) {
+    for (int a = 0; a < 3; ++a) {
+      srt[a].resize(n);
+      for (uint32_t i = 0; i < n; ++i) srt[a][i] = i;
+      std::sort(srt[a].begin(), srt[a].end(), [&](uint32_t x, uint32_t y) {
+        const float cx = centroid[3 * x + a], cy = centroid[3 * y + a];
+        return cx < cy || (cx == cy && x < y);
+      });
+    }
+    tmp.resize(n);
+    side.resize(n);
+    racc.resize(n);
+  }
+
+  void split_full(uint32_t first, uint32_t count, int axis, uint32_t k) {
+    for (uint32_t i = 0; i < count; ++i) side[srt[axis][first + i]] = i < k ? 0 : 1;
+    for (int a = 0; a < 3; ++a) {
+      if (a == axis) continue;
+      uint32_t* s = &srt[a][first];
+      uint32_t nl = 0, nr = 0;
+      for (uint32_t i = 0; i < count; ++i) {
+        if (side[s[i]] == 0) s[nl++] = s[i];
+        else tmp[nr++] = s[i];
+      }
+      std::copy(tmp.begin(), tmp.begin() + nr, s + nl);
+    }
+  }
+
+  int32_t build_full(uint32_t first, uint32_t count, uint32_t depth) {
+    const int32_t id = (int32_t)nodes.size();
+    nodes.emplace_back();
+    Box box;
+    for (uint32_t i = first; i < first + count; ++i) box.grow(prim_box[srt[0][i]]);
+    nodes[id].box = box;
+    nodes[id].depth = depth;
+    const bool depth_limited = depth + 1 >= (uint32_t)kMaxBvhDepth;
+    if (count <= 1 || (depth_limited && count <= (uint32_t)kMaxLeafSize)) return leaf_full(id, first, count, depth);
+    int best_axis = -1;
+    uint32_t best_k = 0;
+    float best_cost = FLT_MAX;
+    for (int axis = 0; axis < 3; ++axis) {
+      const uint32_t* s = &srt[axis][first];
+      Box acc;
+      for (uint32_t k = count; k-- > 1;) { acc.grow(prim_box[s[k]]); racc[k] = acc.area(); }
+      acc = Box();
+      for (uint32_t k = 0; k + 1 < count; ++k) {
+        acc.grow(prim_box[s[k]]);
+        const float cost = acc.area() * (float)(k + 1) + racc[k + 1] * (float)(count - k - 1);
+        if (cost < best_cost) { best_cost = cost; best_axis = axis; best_k = k + 1; }
+      }
+    }
+    const float parent_area = box.area();
+    const float split_cost = parent_area > 0.0f ? opt.traversal_cost + best_cost / parent_area : FLT_MAX;
+    if (count <= opt.max_leaf_size && (float)count <= split_cost) return leaf_full(id, first, count, depth);
+    if (depth_limited) err = "BVH depth limit reached with an oversize leaf";
+    if (best_axis < 0 || depth_limited) { best_axis = 0; best_k = count / 2; }
+    split_full(first, count, best_axis, best_k);
+    const int32_t l = build_full(first, best_k, depth + 1);
+    const int32_t r = build_full(first + best_k, count - best_k, depth + 1);
+    nodes[id].child[0] = l;
+    nodes[id].child[1] = r;
+    return id;
+  }
+
+  int32_t leaf_full(int32_t id, uint32_t first, uint32_t count, uint32_t depth) {
+    nodes[id].first = first;
+    nodes[id].count = count;
+    max_depth = std::max(max_depth, depth);
+    return id;
+  }
+
   void make_leaf(int32_t id, uint32_t first, uint32_t count, uint32_t depth) {
     // leaves hold at most kMaxLeafSize triangles; larger ranges become a
     // small subtree of full leaves (only reachable when centroids coincide)
@@ -498,7 +580,13 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
     b.order[t] = t;
   }
   b.nodes.reserve(2 * (size_t)num_triangles / std::max<uint32_t>(1, opt.max_leaf_size) + 16);
-  b.build(0, num_triangles, 0);
+  if (opt.full_sweep) {
+    b.init_full(num_triangles);
+    b.build_full(0, num_triangles, 0);
+    b.order = b.srt[0];
+  } else {
+    b.build(0, num_triangles, 0);
+  }
   if (!b.err.empty()) { error = b.err; return false; }
   if (opt.width == 8) {
     if (!emit_bvh8(b.nodes, b.prim_box, b.order, positions, stride, indices, num_triangles, opt, out, error)) return false;
