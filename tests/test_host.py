@@ -129,6 +129,25 @@ def test_bvh_procedural_mesh(mrt_mod):
     assert e["vertices"].tobytes() == e2["vertices"].tobytes()
 
 
+def test_full_sweep_sah_builder(mrt_mod, monkeypatch):
+    """Scenes of >= 64 K triangles use the presorted full-sweep SAH builder
+    (bvh.cpp build_full): a valid tree (every primitive in one leaf, boxes
+    contain their triangles, depth within the stack) of lower SAH cost than the
+    binned builder (MRT_FULL_SWEEP=0) on the same mesh; deterministic."""
+    costs = {}
+    for full in ("1", "0"):
+        monkeypatch.setenv("MRT_FULL_SWEEP", full)
+        s = mrt_mod.Scene("cornellbox", device=-1, procedural_triangles=1 << 16, procedural_seed=5)
+        s.check_bvh()
+        costs[full] = (s.info["bvh_sah_cost"], s.info["bvh_nodes"], s.info["bvh_max_stack"])
+        s.close()
+    assert costs["1"][0] < costs["0"][0]
+    monkeypatch.setenv("MRT_FULL_SWEEP", "1")
+    s = mrt_mod.Scene("cornellbox", device=-1, procedural_triangles=1 << 16, procedural_seed=5)
+    assert (s.info["bvh_sah_cost"], s.info["bvh_nodes"], s.info["bvh_max_stack"]) == costs["1"]
+    s.close()
+
+
 def test_mtl_override_glass_variant(mrt_mod, tmp_path):
     """BASELINE C3 glass variant: Ks 0 0 +1.5 instantiates MATERIAL_SMOOTH_DIELECTRIC."""
     src = open(mrt_mod.scene_path("CornellBox-Water-plastic")[:-4] + ".mtl").read()
