@@ -26,7 +26,7 @@ struct BvhBuildOptions {
   uint32_t lds_node_budget = 256; // interior nodes placed first in BFS order
   uint32_t bins = 32;             // SAH bins: 32 measured C3 +1.9 % over 16 (C2, C4 =), 64 C2 -2 %
   uint32_t exact_sah_below = 0;   // ranges of fewer triangles use the exact sweep SAH (0 = never; measured C2 -2 %)
-  bool full_sweep = false;        // exact sweep SAH at every node (presorted, O(n log n)); scenes >= 64 K triangles
+  bool full_sweep = false;        // exact sweep SAH at every node (presorted, O(n log n)); opt-in (MRT_FULL_SWEEP=1)
   float traversal_cost = 1.0f;    // relative to one triangle test
   uint32_t width = 2;             // 2 = BVH2 (64-B nodes), 4 = BVH4 (128-B nodes, collapsed BVH2)
 };

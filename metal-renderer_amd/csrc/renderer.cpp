@@ -595,18 +595,17 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   else if (desc->lds_nodes) opt.lds_node_budget = desc->lds_nodes;
   else opt.lds_node_budget = 256;   // BFS prefix; the launcher stages what fits (fit_lds_nodes)
   if (const char* v = std::getenv("MRT_LDS_NODES"); v && !desc->lds_nodes) opt.lds_node_budget = (uint32_t)std::strtoul(v, nullptr, 0);
-  // large scenes (traversed from global memory): the exact sweep SAH at every
-  // node (presorted, O(n log n)) instead of 32 bins — C4's SAH cost 22.3 ->
-  // 19.1; binned 64 + exact below 64 K measured C4 1822 -> 1935 Mpaths/s
-  // (+6.2 %); C3 / C3g (7 K triangles) unchanged by finer SAH
-  // (tools/env_sweep.sh, r2).  MRT_FULL_SWEEP=0 keeps the binned builder.
+  // large scenes (traversed from global memory): a finer SAH — 64 bins, and
+  // the exact sweep for ranges below 64 K triangles: C4 1822 -> 1925-1935
+  // Mpaths/s (+5.7 %, SAH cost 22.3 -> 20.5), C3 / C3g (7 K triangles) unchanged
+  // (tools/env_sweep.sh, r2).  The presorted full sweep at every node
+  // (MRT_FULL_SWEEP=1: SAH cost 19.0, the fastest build) measured C4 -1.1 %,
+  // C5 share -1.0 %, C2 -2.5 % against it, so it is opt-in.
   if (T >= 65536) {
-    const char* v = std::getenv("MRT_FULL_SWEEP");
-    opt.full_sweep = !v || std::atoi(v) != 0;
     opt.bins = 64;
     opt.exact_sah_below = 65536;
   }
-  if (const char* v = std::getenv("MRT_FULL_SWEEP"); v && T < 65536) opt.full_sweep = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MRT_FULL_SWEEP")) opt.full_sweep = std::atoi(v) != 0;
   // tuning overrides (profiling): MRT_LEAF = max leaf size, MRT_CTRAV = SAH node cost
   if (const char* v = std::getenv("MRT_LEAF")) opt.max_leaf_size = (uint32_t)std::strtoul(v, nullptr, 0);
   if (const char* v = std::getenv("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
