@@ -167,3 +167,107 @@ def test_packet_bruteforce_equals_per_ray(oracle_mod, mrt_mod):
     (i1, (img1, a1)), (i2, (img2, a2)) = out[1 << 40], out[0]
     assert i1.tobytes() == i2.tobytes() and (i1["distance"] > 0).mean() > 0.3
     assert img1.tobytes() == img2.tobytes() and a1 == a2
+
+
+# ------------------------------------------- specular BSDFs: known answers
+# The Water goldens cannot pin the plastic / mirror / dielectric branches
+# (their Mitsuba XML differs from the MTL the reference renders, SURVEY.md
+# App. B), so these pin them against values derived by hand from the
+# reference formulas (renderer/KernelHelpers.h:7-21 fresnel, :116-179
+# generateNextBounce, :56-114 sampleMaterial; renderer/Shaders.metal:199-211
+# next ray): one ray at 45 degrees onto a floor triangle of each BSDF,
+# through the oracle's intersectionHandler stage.
+_KD = np.float32([0.5, 0.6, 0.7])
+_PI_REF = 3.1415926   # Raytracing.h: PI truncated
+
+
+def _fresnel64(cos_i, eta_out, eta_in):
+    eta = eta_out / eta_in
+    sin2 = eta * eta * (1.0 - cos_i * cos_i)
+    if sin2 >= 1.0:
+        return 1.0
+    cos_t = np.sqrt(1.0 - sin2)
+    rs = (eta_in * cos_i - eta_out * cos_t) / (eta_in * cos_i + eta_out * cos_t)
+    rp = (eta_in * cos_t - eta_out * cos_i) / (eta_in * cos_t + eta_out * cos_i)
+    return 0.5 * (rs * rs + rp * rp)
+
+
+def _shade_one(oracle_mod, mtype, ior, noise4, current_ior=1.00029):
+    V = np.zeros(6, oracle_mod.VERTEX_DTYPE)
+    V["v"] = [(1, 0, 0), (1, 0, -1), (0, 0, 0), (-1, 2, -1), (1, 2, -1), (0, 2, 1)]
+    V["n"] = [(0, 1, 0)] * 3 + [(0, -1, 0)] * 3
+    M = np.zeros(2, oracle_mod.MATERIAL_DTYPE)
+    M[0] = (_KD, (0, 0, 0), ior, mtype)
+    M[1] = ((0, 0, 0), (1, 1, 1), 0.0, 0)
+    R = np.zeros(2, oracle_mod.TRIREF_DTYPE)
+    R["tri"] = [(0, 1, 2), (3, 4, 5)]
+    R["materialIndex"] = [0, 1]
+    sc = oracle_mod.OracleScene.from_arrays(V, R, M)
+    d = np.float32([1, -1, 0]) / np.float32(np.sqrt(2))
+    ray = np.zeros(1, oracle_mod.RAY_DTYPE)
+    ray["origin"] = (0, 1, 0)
+    ray["direction"] = d
+    ray["maxDistance"] = np.inf
+    ray["throughput"] = (1, 1, 1)
+    ray["params"] = (1.0, 0.0, 1.0, current_ior)   # bounce 1 of L = 4: NEE on
+    isect = np.zeros(1, oracle_mod.ISECT_DTYPE)
+    isect["distance"] = np.sqrt(2)
+    isect["triangleIndex"] = 0
+    isect["coordinates"] = (1.0, 0.0)          # the hit is V0 = (1, 0, 0), n = (0, 1, 0)
+    srays = np.zeros(1, oracle_mod.SRAY_DTYPE)
+    noise = np.tile(np.float32(noise4), 64 * 64)
+    sc.shade(1, 1, 0, 4, noise, isect, ray, srays)
+    return ray[0], srays[0], d.astype(np.float64)
+
+
+def _assert_mirror(ray, d, ior_in):
+    c = 1.0 / np.sqrt(2.0)
+    np.testing.assert_allclose(ray["direction"], [c, c, 0.0], rtol=1e-6, atol=1e-7)   # reflect(wI, n)
+    np.testing.assert_allclose(ray["throughput"], _KD * c, rtol=1e-6)                 # Kd * cos / 1
+    np.testing.assert_allclose(ray["params"], [1.0, 0.0, 2.0, ior_in], rtol=1e-6)     # pdf 1, not diffuse
+
+
+def test_mirror_bsdf_known_answer(oracle_mod):
+    ray, sray, d = _shade_one(oracle_mod, 1, 0.0, (0.3, 0.5, 0.25, 0.64))
+    _assert_mirror(ray, d, np.float32(1.00029))
+    np.testing.assert_allclose(ray["origin"], [1.0, 1e-4, 0.0], rtol=1e-6, atol=1e-9)   # p + n * 1e-4
+    np.testing.assert_array_equal(sray["throughput"], [0, 0, 0])   # NEE never samples a delta lobe
+
+
+@pytest.mark.parametrize("mtype", [2, 3])
+def test_fresnel_selects_the_lobe_at_the_exact_value(oracle_mod, mtype):
+    """Plastic (2) and dielectric (3): the lobe flips from mirror to
+    diffuse / pass-through exactly where noise.y crosses the unpolarised
+    Fresnel reflectance (45 degrees, IoR 1.00029 -> 1.5)."""
+    F = _fresnel64(1.0 / np.sqrt(2.0), 1.00029, 1.5)
+    assert 0.04 < F < 0.06
+    below, _, d = _shade_one(oracle_mod, mtype, 1.5, (0.3, F * (1 - 1e-4), 0.25, 0.64))
+    _assert_mirror(below, d, np.float32(1.00029))
+    above, sray, d = _shade_one(oracle_mod, mtype, 1.5, (0.3, F * (1 + 1e-4), 0.25, 0.64))
+    if mtype == 3:   # pass straight through, carrying the material's IoR
+        np.testing.assert_allclose(above["direction"], d, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(above["throughput"], _KD, rtol=1e-6)
+        np.testing.assert_allclose(above["params"], [1.0, 0.0, 2.0, 1.5], rtol=1e-6)
+        np.testing.assert_array_equal(sray["throughput"], [0, 0, 0])   # sampleMaterial: 0 for F < noise.y
+    else:            # the diffuse lobe: cosine-weighted around n, but NOT flagged diffuse (App. B)
+        cos_t, phi = np.sqrt(0.64), 0.25 * 2.0 * _PI_REF
+        want = [np.cos(phi) * 0.6, cos_t, -np.sin(phi) * 0.6]   # basis u = (1,0,0), v = (0,0,-1) for n = +y
+        np.testing.assert_allclose(above["direction"], want, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(above["throughput"], _KD, rtol=1e-6)   # bsdf == pdf
+        np.testing.assert_allclose(above["params"], [cos_t / _PI_REF, 0.0, 2.0, 1.00029], rtol=1e-6)
+
+
+def test_total_internal_reflection_is_a_mirror(oracle_mod):
+    """Inside a denser medium at 45 degrees (IoR 1.5 -> 1.0): sin^2 > 1,
+    fresnel returns 1, so even noise.y = 0.999 reflects."""
+    assert _fresnel64(1.0 / np.sqrt(2.0), 1.5, 1.0) == 1.0
+    ray, _, d = _shade_one(oracle_mod, 3, 1.0, (0.3, 0.999, 0.25, 0.64), current_ior=1.5)
+    _assert_mirror(ray, d, np.float32(1.5))
+
+
+def test_diffuse_bsdf_known_answer(oracle_mod):
+    ray, _, _ = _shade_one(oracle_mod, 0, 0.0, (0.3, 0.5, 0.25, 0.64))
+    cos_t, phi = 0.8, 0.25 * 2.0 * _PI_REF
+    np.testing.assert_allclose(ray["direction"], [np.cos(phi) * 0.6, cos_t, -np.sin(phi) * 0.6], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(ray["throughput"], _KD, rtol=1e-6)
+    np.testing.assert_allclose(ray["params"], [cos_t / _PI_REF, 1.0, 2.0, 1.00029], rtol=1e-6)
