@@ -284,3 +284,44 @@ def test_exr_reader_formats(mrt_mod, tmp_path, comp, ptype):
     assert np.array_equal(got[::-1, :, :3], rgb) and np.array_equal(got[..., :3], exr.read_rgb(p)[::-1])
     with pytest.raises(mrt_mod.MrtError, match="OpenEXR|open"):
         mrt_mod.load_exr(str(tmp_path / "missing.exr"))
+
+
+@pytest.mark.parametrize("L", [2, 4, 8])
+def test_stream_kernel_level_bound(L):
+    """kernels.hip::stream_kernel keeps a wave's queue per bounce level in
+    kStreamCap = 128 slots.  Its schedule — run the deepest level holding
+    >= 64 rays, else up to 64 camera rays, else (camera rays exhausted) the
+    deepest non-empty level; survivors append to the next level — must never
+    hold more than 127 rays in a level, for any survivor pattern.  A
+    restatement of the schedule driven by random and adversarial survivor
+    counts (every ray survives, none do, bursts) checks the bound and that
+    every ray is run exactly once per bounce it reaches."""
+    rng = np.random.default_rng(L)
+    for trial in range(200):
+        cam = int(rng.integers(1, 3000))
+        mode = trial % 4
+        cnt = [0] * L
+        pend = cam
+        runs = [0] * L   # rays run per bounce
+        alive = [0] * L  # survivors of bounce b
+        while True:
+            lvl = next((k for k in range(L - 1, 0, -1) if cnt[k] >= 64), 0)
+            if lvl == 0 and pend > 0:
+                n = min(64, pend)
+                pend -= n
+            else:
+                if lvl == 0:
+                    lvl = next((k for k in range(L - 1, 0, -1) if cnt[k] > 0), 0)
+                    if lvl == 0:
+                        break
+                n = min(64, cnt[lvl])
+                cnt[lvl] -= n
+            runs[lvl] += n
+            if lvl + 1 < L:
+                s = n if mode == 0 else 0 if mode == 1 else (n if rng.random() < 0.5 else 0) if mode == 2 \
+                    else int(rng.integers(0, n + 1))
+                cnt[lvl + 1] += s
+                alive[lvl] += s
+                assert cnt[lvl + 1] <= 127, (L, trial, cnt)
+        assert runs[0] == cam
+        assert all(runs[b + 1] == alive[b] for b in range(L - 1))
