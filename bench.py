@@ -407,6 +407,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "achieved_is": "algorithmic bytes per launch / launch time (equivalent bandwidth)",
+                     "frac_note": "SURVEY 8(d) algorithmic bytes (the reference's 2+4L-pass wavefront traffic); "
+                                  "the fused kernel moves far fewer, so frac can exceed 1 - counter.hbm_frac is the "
+                                  "measured HBM rate",
                      "counter": counter,
                      "limiter": "VALU issue + memory latency of BVH traversal (not HBM bandwidth)",
                      "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),
