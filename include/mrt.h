@@ -72,7 +72,7 @@ typedef struct mrt_scene_desc {
   uint32_t max_leaf_size;          /* BVH leaf size, 0 = default (2) */
   uint32_t lds_nodes;              /* top BVH nodes staged in LDS, 0 = default; UINT32_MAX = none */
   int device;                      /* HIP device ordinal; -1 = host only (import + BVH, no upload) */
-  uint32_t bvh_width;              /* 2 = BVH2, 4 = BVH4 (collapsed BVH2), 0 = default (4) */
+  uint32_t bvh_width;              /* 4 = BVH4 (the binary SAH tree collapsed), 0 = default (4); other widths are rejected */
   uint32_t bvh_builder;            /* MRT_BVH_*; 0 = default (host binned SAH) */
 } mrt_scene_desc;
 

@@ -275,295 +275,12 @@ inline void padded_box(const Box& bx, float lo[3], float hi[3]) {
   }
 }
 
-// ---- compressed 8-wide BVH (mrt_layout.h "BVH8") ---------------------------
-// Built from the binary SAH tree: a node's children are found by repeatedly
-// opening the largest-area openable child (an interior subtree of more than
-// kBvh8LeafTris triangles, or an oversize leaf range, split in half) until 8
-// children exist; a subtree of <= kBvh8LeafTris triangles becomes one leaf
-// slot.  Nodes are emitted breadth first (the top levels first, for LDS
-// staging; a node's interior children are consecutive nodes, its leaf
-// triangles a consecutive run), child boxes quantised to 8 bits against the
-// node's origin and per-axis power-of-two scale, rounded outward and checked
-// in float with the kernel's own arithmetic (plane = p + 2^e * q), and the
-// children placed in the 8 slots by the octant their centroid lies in
-// relative to the node centre, so a ray visits slot (k ^ ray octant) k-th:
-// an approximately near-to-far order without sorting.
-constexpr uint32_t kBvh8LeafTris = 3;
-
-struct Item {
-  int32_t id;          // build node, or -1 for a part of a split leaf range
-  uint32_t first, count;
-  Box box;
-  bool leaf;           // emitted as a leaf slot (<= kBvh8LeafTris triangles), else as a child node
-};
-
-struct Bvh8Emitter {
-  const std::vector<BuildNode>& bn;
-  const std::vector<Box>& prim_box;
-  const std::vector<uint32_t>& order;
-  std::vector<uint32_t> sub_first, sub_count;   // subtree triangle range of each build node (contiguous in `order`)
-
-  Bvh8Emitter(const std::vector<BuildNode>& n, const std::vector<Box>& pb, const std::vector<uint32_t>& o)
-      : bn(n), prim_box(pb), order(o), sub_first(n.size()), sub_count(n.size()) {
-    std::vector<int32_t> st{0}, post;
-    while (!st.empty()) {
-      const int32_t k = st.back();
-      st.pop_back();
-      post.push_back(k);
-      if (bn[k].child[0] >= 0) { st.push_back(bn[k].child[0]); st.push_back(bn[k].child[1]); }
-    }
-    for (size_t i = post.size(); i-- > 0;) {
-      const int32_t k = post[i];
-      if (bn[k].child[0] < 0) { sub_first[k] = bn[k].first; sub_count[k] = bn[k].count; continue; }
-      const int32_t l = bn[k].child[0], r = bn[k].child[1];
-      sub_first[k] = std::min(sub_first[l], sub_first[r]);
-      sub_count[k] = sub_count[l] + sub_count[r];
-    }
-  }
-  Item item_of(int32_t id) const {
-    return Item{id, sub_first[id], sub_count[id], bn[id].box, sub_count[id] <= kBvh8LeafTris};
-  }
-  Item range_item(uint32_t first, uint32_t count) const {
-    Item it{-1, first, count, Box(), count <= kBvh8LeafTris};
-    for (uint32_t i = first; i < first + count; ++i) it.box.grow(prim_box[order[i]]);
-    return it;
-  }
-  void open(const Item& it, Item& a, Item& b) const {
-    if (it.id >= 0 && bn[it.id].child[0] >= 0) { a = item_of(bn[it.id].child[0]); b = item_of(bn[it.id].child[1]); return; }
-    const uint32_t h = it.count / 2;   // an oversize leaf range: halves
-    a = range_item(it.first, h);
-    b = range_item(it.first + h, it.count - h);
-  }
-  // the children of a node item (the root of a tiny scene may be one leaf)
-  std::vector<Item> collapse(const Item& node) const {
-    if (node.leaf) return {node};
-    Item a, b;
-    open(node, a, b);
-    std::vector<Item> ch{a, b};
-    while (ch.size() < 8) {
-      int best = -1;
-      float best_area = -1.0f;
-      for (size_t i = 0; i < ch.size(); ++i)
-        if (!ch[i].leaf && ch[i].box.area() > best_area) { best = (int)i; best_area = ch[i].box.area(); }
-      if (best < 0) break;
-      Item x, y;
-      open(ch[best], x, y);
-      ch[best] = x;
-      ch.push_back(y);
-    }
-    return ch;
-  }
-};
-
-// float plane of quantised coordinate q: exactly what the kernels compute
-// (2^e * q is exact for q <= 255; one rounding in the add)
-inline float q_plane(float p, int e, uint32_t q) { return p + std::ldexp((float)q, e); }
-
-bool emit_bvh8(const std::vector<BuildNode>& bn, const std::vector<Box>& prim_box, const std::vector<uint32_t>& order,
-               const float* positions, size_t stride, const uint32_t* indices, uint32_t num_triangles,
-               const BvhBuildOptions& opt, BvhResult& out, std::string& error) {
-  Bvh8Emitter em(bn, prim_box, order);
-  auto P = [&](uint32_t vi) { return positions + (size_t)vi * stride; };
-  struct Pending { Item item; uint32_t level; };
-  std::vector<Pending> q;          // BFS queue = node output order
-  q.push_back({em.item_of(0), 0});
-  out.nodes.clear();
-  out.tris.assign(12 * (size_t)num_triangles, 0.0f);
-  uint32_t tri_cursor = 0;
-  double sah = 0.0;
-  const double root_area = std::max(1e-30, (double)bn[0].box.area());
-  uint32_t max_level = 0;
-  for (size_t k = 0; k < q.size(); ++k) {
-    const Item node = q[k].item;
-    const uint32_t level = q[k].level;
-    max_level = std::max(max_level, level);
-    std::vector<Item> ch = em.collapse(node);
-    sah += opt.traversal_cost * node.box.area() / root_area;
-    // octant slots: child c goes to the free slot whose sign pattern best
-    // matches its centroid offset from the node centre (greedy by score)
-    float ctr[3];
-    for (int a = 0; a < 3; ++a) ctr[a] = 0.5f * (node.box.lo[a] + node.box.hi[a]);
-    struct Cand { float score; int c, s; };
-    std::vector<Cand> cand;
-    for (int c = 0; c < (int)ch.size(); ++c)
-      for (int s = 0; s < 8; ++s) {
-        float sc = 0.0f;
-        for (int a = 0; a < 3; ++a) {
-          const float d = 0.5f * (ch[c].box.lo[a] + ch[c].box.hi[a]) - ctr[a];
-          sc += ((s >> a) & 1) ? d : -d;
-        }
-        cand.push_back({sc, c, s});
-      }
-    std::stable_sort(cand.begin(), cand.end(), [](const Cand& x, const Cand& y) { return x.score > y.score; });
-    int slot_child[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-    std::vector<int> child_slot(ch.size(), -1);
-    for (const Cand& cd : cand)
-      if (slot_child[cd.s] < 0 && child_slot[cd.c] < 0) { slot_child[cd.s] = cd.c; child_slot[cd.c] = cd.s; }
-    // node record
-    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-    std::vector<std::array<float, 6>> cbox(ch.size());
-    for (size_t c = 0; c < ch.size(); ++c) {
-      padded_box(ch[c].box, &cbox[c][0], &cbox[c][3]);
-      for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], cbox[c][a]); hi[a] = std::max(hi[a], cbox[c][3 + a]); }
-    }
-    int e[3];
-    for (int a = 0; a < 3; ++a) {
-      const double ext = (double)hi[a] - (double)lo[a];
-      e[a] = ext > 0.0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
-      e[a] = std::max(-100, std::min(100, e[a]));
-      while (q_plane(lo[a], e[a], 255) < hi[a]) ++e[a];
-    }
-    const uint32_t node_index = (uint32_t)k;
-    out.nodes.resize(20 * ((size_t)node_index + 1), 0.0f);
-    float* o = &out.nodes[20 * (size_t)node_index];
-    uint32_t imask = 0;
-    uint8_t meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint8_t qlo[3][8], qhi[3][8];
-    for (int a = 0; a < 3; ++a)
-      for (int s = 0; s < 8; ++s) { qlo[a][s] = 255; qhi[a][s] = 0; }   // empty slot: inverted box
-    const uint32_t child_base = (uint32_t)q.size();
-    const uint32_t tri_base = tri_cursor;
-    for (int s = 0; s < 8; ++s) {
-      const int c = slot_child[s];
-      if (c < 0) continue;
-      for (int a = 0; a < 3; ++a) {
-        const double sc = std::ldexp(1.0, e[a]);
-        int ql = (int)std::floor(((double)cbox[c][a] - (double)lo[a]) / sc);
-        int qh = (int)std::ceil(((double)cbox[c][3 + a] - (double)lo[a]) / sc);
-        ql = std::max(0, std::min(255, ql));
-        qh = std::max(0, std::min(255, qh));
-        while (ql > 0 && q_plane(lo[a], e[a], (uint32_t)ql) > cbox[c][a]) --ql;
-        while (qh < 255 && q_plane(lo[a], e[a], (uint32_t)qh) < cbox[c][3 + a]) ++qh;
-        if (q_plane(lo[a], e[a], (uint32_t)ql) > cbox[c][a] || q_plane(lo[a], e[a], (uint32_t)qh) < cbox[c][3 + a]) {
-          error = "internal: BVH8 quantisation not conservative";
-          return false;
-        }
-        qlo[a][s] = (uint8_t)ql;
-        qhi[a][s] = (uint8_t)qh;
-      }
-      if (!ch[c].leaf) {
-        imask |= 1u << s;
-      } else {
-        const uint32_t off = tri_cursor - tri_base, cnt = ch[c].count;
-        if (cnt == 0 || cnt > kBvh8LeafTris || off + cnt > 24) { error = "internal: BVH8 leaf slot overflow"; return false; }
-        meta[s] = (uint8_t)((((1u << cnt) - 1u) << 5) | off);
-        for (uint32_t i = 0; i < cnt; ++i) {
-          const uint32_t prim = order[ch[c].first + i];
-          const float* v0 = P(indices[3 * prim]);
-          const float* v1 = P(indices[3 * prim + 1]);
-          const float* v2 = P(indices[3 * prim + 2]);
-          float* t = &out.tris[12 * (size_t)(tri_cursor + i)];
-          t[0] = v0[0]; t[1] = v0[1]; t[2] = v0[2]; t[3] = bitsf(prim);
-          t[4] = v1[0] - v0[0]; t[5] = v1[1] - v0[1]; t[6] = v1[2] - v0[2]; t[7] = 0.0f;
-          t[8] = v2[0] - v0[0]; t[9] = v2[1] - v0[1]; t[10] = v2[2] - v0[2]; t[11] = 0.0f;
-        }
-        tri_cursor += cnt;
-        out.num_leaves++;
-        sah += (double)cnt * ch[c].box.area() / root_area;
-      }
-    }
-    // interior children: consecutive nodes in slot order (queued now, so
-    // their output indices are child_base + rank)
-    for (int s = 0; s < 8; ++s)
-      if (imask & (1u << s)) q.push_back({ch[slot_child[s]], level + 1});
-    o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2];
-    o[3] = bitsf((uint32_t)(e[0] + 128) | ((uint32_t)(e[1] + 128) << 8) | ((uint32_t)(e[2] + 128) << 16) | (imask << 24));
-    o[4] = bitsf(child_base);
-    o[5] = bitsf(tri_base);
-    uint32_t m0 = 0, m1 = 0;
-    for (int s = 0; s < 4; ++s) { m0 |= (uint32_t)meta[s] << (8 * s); m1 |= (uint32_t)meta[4 + s] << (8 * s); }
-    o[6] = bitsf(m0);
-    o[7] = bitsf(m1);
-    for (int a = 0; a < 3; ++a) {
-      uint32_t l0 = 0, l1 = 0, h0 = 0, h1 = 0;
-      for (int s = 0; s < 4; ++s) {
-        l0 |= (uint32_t)qlo[a][s] << (8 * s); l1 |= (uint32_t)qlo[a][4 + s] << (8 * s);
-        h0 |= (uint32_t)qhi[a][s] << (8 * s); h1 |= (uint32_t)qhi[a][4 + s] << (8 * s);
-      }
-      o[8 + 2 * a] = bitsf(l0); o[9 + 2 * a] = bitsf(l1);      // qlo.x, qlo.y, qlo.z at [8..13]
-      o[14 + 2 * a] = bitsf(h0); o[15 + 2 * a] = bitsf(h1);    // qhi.x, qhi.y, qhi.z at [14..19]
-    }
-  }
-  if (tri_cursor != num_triangles) { error = "internal: BVH8 triangle count mismatch"; return false; }
-  out.num_nodes = (uint32_t)q.size();
-  out.root = 0;
-  out.width = 8;
-  out.wide_depth = max_level + 1;
-  // each node step pushes at most the rest of its group: one entry per level
-  out.max_stack = max_level + 1;
-  out.lds_nodes = std::min<uint32_t>(opt.lds_node_budget, out.num_nodes);
-  out.sah_cost = sah;
-  return true;
-}
-
-// per-axis exponent of a node's quantisation grid: 255 steps of 2^e from lo
-// reach hi (in float, as the kernels compute planes)
-inline int grid_exponent(float lo, float hi) {
-  const double ext = (double)hi - (double)lo;
-  int e = ext > 0.0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
-  e = std::max(-100, std::min(100, e));
-  while (q_plane(lo, e, 255) < hi) ++e;
-  return e;
-}
-
-// outward-rounded 8-bit planes of [clo, chi] on the grid (lo, e), checked in float
-inline bool quantize_span(float lo, int e, float clo, float chi, uint32_t& ql_out, uint32_t& qh_out) {
-  const double sc = std::ldexp(1.0, e);
-  int ql = (int)std::floor(((double)clo - (double)lo) / sc);
-  int qh = (int)std::ceil(((double)chi - (double)lo) / sc);
-  ql = std::max(0, std::min(255, ql));
-  qh = std::max(0, std::min(255, qh));
-  while (ql > 0 && q_plane(lo, e, (uint32_t)ql) > clo) --ql;
-  while (qh < 255 && q_plane(lo, e, (uint32_t)qh) < chi) ++qh;
-  ql_out = (uint32_t)ql;
-  qh_out = (uint32_t)qh;
-  return q_plane(lo, e, (uint32_t)ql) <= clo && q_plane(lo, e, (uint32_t)qh) >= chi;
-}
-
 }  // namespace
-
-bool quantize_bvh4(const std::vector<float>& nodes, uint32_t num_nodes, std::vector<float>& qnodes,
-                   std::string& error) {
-  if (nodes.size() < 32 * (size_t)num_nodes) { error = "quantize_bvh4: not a BVH4 node array"; return false; }
-  qnodes.assign(16 * (size_t)std::max<uint32_t>(1, num_nodes), 0.0f);
-  for (uint32_t k = 0; k < num_nodes; ++k) {
-    const float* n = &nodes[32 * (size_t)k];
-    float* o = &qnodes[16 * (size_t)k];
-    bool live[4];
-    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-    for (int c = 0; c < 4; ++c) {
-      live[c] = fbits(n[24 + c]) != (uint32_t)kEmptyChild;
-      if (!live[c]) continue;
-      for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], n[8 * a + c]); hi[a] = std::max(hi[a], n[8 * a + 4 + c]); }
-    }
-    int e[3] = {0, 0, 0};
-    for (int a = 0; a < 3; ++a) {
-      if (lo[a] > hi[a]) lo[a] = hi[a] = 0.0f;   // no live child (not emitted by the builders)
-      e[a] = grid_exponent(lo[a], hi[a]);
-    }
-    uint32_t w[6] = {0, 0, 0, 0, 0, 0};   // qlo.x, qhi.x, qlo.y, qhi.y, qlo.z, qhi.z; byte c = child c
-    for (int c = 0; c < 4; ++c)
-      for (int a = 0; a < 3; ++a) {
-        uint32_t ql = 255, qh = 0;   // empty slot: inverted box
-        if (live[c] && !quantize_span(lo[a], e[a], n[8 * a + c], n[8 * a + 4 + c], ql, qh)) {
-          error = "internal: quantised BVH4 box not conservative";
-          return false;
-        }
-        w[2 * a] |= ql << (8 * c);
-        w[2 * a + 1] |= qh << (8 * c);
-      }
-    o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2];
-    o[3] = bitsf((uint32_t)(e[0] + 128) | ((uint32_t)(e[1] + 128) << 8) | ((uint32_t)(e[2] + 128) << 16));
-    for (int c = 0; c < 4; ++c) o[4 + c] = n[24 + c];
-    for (int i = 0; i < 6; ++i) o[8 + i] = bitsf(w[i]);
-  }
-  return true;
-}
 
 bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indices, uint32_t num_triangles,
                const BvhBuildOptions& opt, BvhResult& out, std::string& error) {
   if (num_triangles == 0) { error = "empty scene"; return false; }
-  if (opt.width != 2 && opt.width != 4 && opt.width != 8) { error = "BVH width must be 2, 4 or 8"; return false; }
+  if (opt.width != 2 && opt.width != 4) { error = "BVH width must be 2 or 4"; return false; }
   if (opt.max_leaf_size == 0 || opt.max_leaf_size > (uint32_t)kMaxLeafSize) { error = "bad leaf size"; return false; }
   if (num_triangles >= (1u << (31 - kLeafCountBits))) { error = "too many triangles"; return false; }
   Builder b(opt);
@@ -588,12 +305,6 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
     b.build(0, num_triangles, 0);
   }
   if (!b.err.empty()) { error = b.err; return false; }
-  if (opt.width == 8) {
-    if (!emit_bvh8(b.nodes, b.prim_box, b.order, positions, stride, indices, num_triangles, opt, out, error)) return false;
-    out.max_depth = b.max_depth;
-    return true;
-  }
-
   // ---- collapse to the output width ----------------------------------------
   // A wide node's children are found by repeatedly opening the largest-area
   // interior child of the binary node (width 2 is the identity).

@@ -28,7 +28,7 @@ struct BvhBuildOptions {
   uint32_t exact_sah_below = 0;   // ranges of fewer triangles use the exact sweep SAH (0 = never; measured C2 -2 %)
   bool full_sweep = false;        // exact sweep SAH at every node (presorted, O(n log n)); opt-in (MRT_FULL_SWEEP=1)
   float traversal_cost = 1.0f;    // relative to one triangle test
-  uint32_t width = 2;             // 2 = BVH2 (64-B nodes), 4 = BVH4 (128-B nodes, collapsed BVH2)
+  uint32_t width = 2;             // 2 = the binary SAH tree itself, 4 = BVH4 (128-B nodes, collapsed; what the kernels traverse)
 };
 
 struct BvhResult {
@@ -48,13 +48,6 @@ struct BvhResult {
 // positions: 3 floats per vertex at `stride_bytes` stride (24 for RefVertex).
 bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indices, uint32_t num_triangles,
                const BvhBuildOptions& opt, BvhResult& out, std::string& error);
-
-// Quantised BVH4 (mrt_layout.h, 16 floats per node) from a BVH4's nodes (32
-// floats per node): same node order, refs and leaves; 64-B instead of 128-B
-// node fetches for the path kernel.  Fails if a quantised box would not
-// contain its child's padded box.
-bool quantize_bvh4(const std::vector<float>& nodes, uint32_t num_nodes, std::vector<float>& qnodes,
-                   std::string& error);
 
 inline int32_t leaf_ref(uint32_t first, uint32_t count) {
   return (int32_t)~((first << kLeafCountBits) | (count - 1));

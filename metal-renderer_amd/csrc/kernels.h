@@ -48,8 +48,6 @@ static_assert(kGrabRanges <= 31, "kGrabRanges");
 #endif
 constexpr uint32_t kGrabStride = MRT_GRAB_STRIDE;    // uint32 words between counters
 constexpr uint32_t kSegSlack = 1024;
-constexpr uint32_t kRefillSlack = 2048;   // segment slack of the lane-refill kernel (kernels.hip)
-constexpr uint32_t kMaxSegSlack = kRefillSlack;
 
 // Wave-local streaming wavefront (stream_kernel): every bounce of a batch in
 // one launch with no inter-wave hand-off.  Each wave keeps its own queue of
@@ -77,13 +75,7 @@ struct BounceArgs {
   // (left a diffuse surface) to [g*cap, g*cap + c0_g) and its class-1
   // survivors to [g*cap + cap - c1_g, g*cap + cap) of the output queue
   // (cap = chunk + kSegSlack); counts are [c0 of all blocks][c1 of all blocks]
-  // lane-refill kernel with classes = 4 (MRT_CLASSES=4, measurement of the
-  // per-BSDF re-sort): one class per material type left (diffuse, mirror,
-  // plastic, dielectric); block g owns two segments of cap slots each,
-  // classes 0/1 at the front/back of [2g*cap, 2g*cap + cap) and 2/3 of the
-  // next; counts are [c0 of all blocks][c1 ...][c2 ...][c3 ...]
-  uint32_t classes;            // 2 (default) or 4 (lane-refill kernel only)
-  uint32_t in_segments;        // bounce > 0: number of input segments (classes x previous grid size)
+  uint32_t in_segments;        // bounce > 0: number of input segments (2 classes x previous grid size)
   const uint32_t* in_seg_count;
   const uint32_t* in_chunk;    // previous launch's chunk (segment stride in slots)
   uint32_t* out_seg_count;     // [grid]
@@ -99,7 +91,7 @@ struct BounceArgs {
   float4* radiance;            // [batch][num_slots] path radiance by owned slot, written once per
                                // owned pixel when its path ends (accumulated by launch_accumulate_frame)
   uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
-                               // [grid * 256][max_stack (x2 for BVH8)] uint32 (null if none)
+                               // [grid * 256][max_stack] uint32 (null if none)
   uint32_t* bounce_counts;     // path / stream kernel: [max_path_length] rays alive at the start of bounce b + 1
 };
 
@@ -139,7 +131,7 @@ struct AccumArgs {
                           uint32_t grid, hipStream_t s);                                                  \
   hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                   \
   /* wave-local streaming wavefront: all bounces of a batch in one launch, per-wave ray queues     \
-     (whole-scene-in-LDS BVH2/BVH4 scenes; hipErrorNotSupported otherwise) */                          \
+     (whole-scene-in-LDS scenes; hipErrorNotSupported otherwise)     */                          \
   hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
                            uint32_t grid, hipStream_t s);                                                 \
   bool stream_supported(const DeviceScene& sc, uint32_t stack_entries);                                   \

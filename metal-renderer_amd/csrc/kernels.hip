@@ -198,32 +198,6 @@ __device__ __forceinline__ float slab(float p, float o, float inv, float oinv) {
 #endif
 }
 
-// Box test of both children of a node; returns entry distances.
-__device__ __forceinline__ void box2(const float4& a, const float4& b, const float4& c, V3 o, const RayBox& rb,
-                                     float tmin, float tmax, bool& hl, bool& hr, float& tnl, float& tnr) {
-#if MRT_PRECISE
-  const V3 oi = o;
-  const float ox = o.x, oy = o.y, oz = o.z;
-  const float oix = 0.0f, oiy = 0.0f, oiz = 0.0f;
-  (void)oi;
-#else
-  const float ox = 0.0f, oy = 0.0f, oz = 0.0f;
-  const float oix = rb.oinv.x, oiy = rb.oinv.y, oiz = rb.oinv.z;
-#endif
-  const float lx0 = slab(a.x, ox, rb.inv.x, oix), lx1 = slab(a.y, ox, rb.inv.x, oix);
-  const float ly0 = slab(a.z, oy, rb.inv.y, oiy), ly1 = slab(a.w, oy, rb.inv.y, oiy);
-  const float lz0 = slab(c.x, oz, rb.inv.z, oiz), lz1 = slab(c.y, oz, rb.inv.z, oiz);
-  const float rx0 = slab(b.x, ox, rb.inv.x, oix), rx1 = slab(b.y, ox, rb.inv.x, oix);
-  const float ry0 = slab(b.z, oy, rb.inv.y, oiy), ry1 = slab(b.w, oy, rb.inv.y, oiy);
-  const float rz0 = slab(c.z, oz, rb.inv.z, oiz), rz1 = slab(c.w, oz, rb.inv.z, oiz);
-  tnl = fmaxf(fmaxf(fminf(lx0, lx1), fminf(ly0, ly1)), fmaxf(fminf(lz0, lz1), tmin));
-  const float tfl = fminf(fminf(fmaxf(lx0, lx1), fmaxf(ly0, ly1)), fminf(fmaxf(lz0, lz1), tmax));
-  tnr = fmaxf(fmaxf(fminf(rx0, rx1), fminf(ry0, ry1)), fmaxf(fminf(rz0, rz1), tmin));
-  const float tfr = fminf(fminf(fmaxf(rx0, rx1), fmaxf(ry0, ry1)), fminf(fmaxf(rz0, rz1), tmax));
-  hl = tnl <= tfl;
-  hr = tnr <= tfr;
-}
-
 // Box test of the four children of a BVH4 node (component-major node, see
 // mrt_layout.h); returns each child's entry distance, +inf for a miss or an
 // empty slot.  ORDERED: the x and y plane rows arrive as (near, far) (a
@@ -286,8 +260,7 @@ struct LdsCtx {
   uint32_t stack_base;    // uint32 offset of the block's stack slot 0 (lane 0's); lanes add threadIdx.x
   uint32_t* spill;        // stack entries >= STACK: the block's rows of a global [lane][word] spill
                           //   area (null when STACK covers the BVH); lane threadIdx.x's row
-  uint32_t spill_lane;    //   starts threadIdx.x * spill_lane words in (one word per BVH4 entry,
-                          //   two per BVH8 group entry)
+  uint32_t spill_lane;    //   starts threadIdx.x * spill_lane words in (one word per entry)
 };
 
 __device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
@@ -301,7 +274,7 @@ __host__ __device__ constexpr uint32_t node_stride_f4(int mode, uint32_t node_f4
 }
 
 // float4 counts of the staged scene image for a mode
-// (node_f4 = float4s per node: 4 for BVH2, 8 for BVH4)
+// (node_f4 = float4s per BVH4 node: 8)
 __host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t node_f4, uint32_t nodes, uint32_t lds_nodes,
                                                       uint32_t tris, uint32_t mats, uint32_t lights) {
   if (mode == kAllLds) return node_stride_f4(mode, node_f4) * nodes + 3 * tris + 6 * tris + 2 * mats + 7 * lights;
@@ -353,23 +326,6 @@ __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx&
       }
 #endif
     }
-  }
-}
-
-template <int MODE>
-__device__ __forceinline__ void fetch_node(const DeviceScene& sc, const LdsCtx& cx, int32_t node, float4& a,
-                                           float4& b, float4& c, float4& e) {
-  if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
-    a = g_lds[4 * node];
-    b = g_lds[4 * node + 1];
-    c = g_lds[4 * node + 2];
-    e = g_lds[4 * node + 3];
-  } else {
-    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 4 * (size_t)node;
-    a = p[0];
-    b = p[1];
-    c = p[2];
-    e = p[3];
   }
 }
 
@@ -448,7 +404,7 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   const uint32_t f4 = cx.light_base + 7 * NL;
   cx.scratch_base = 4 * f4;
   cx.stack_base = cx.scratch_base + ((scratch_u32 + 3) & ~3u);
-  cx.spill_lane = (sc.width == 8 ? 2u : 1u) * sc.max_stack;
+  cx.spill_lane = sc.max_stack;
   cx.spill = spill ? spill + (size_t)blockIdx.x * kBlock * cx.spill_lane : nullptr;
   if (MODE != kGlobal) {
     const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes), reinterpret_cast<const float4*>(sc.tris),
@@ -482,8 +438,8 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
 // ANY = false: nearest hit in [tmin, h.t]; ties -> lowest primitive index.
 // ANY = true:  stop at the first primitive k != target with (t_k, k) <
 //              (t_target, target) in [0, t_target] (shadow occlusion).
-// Both results are independent of the visiting order, so the BVH2 and BVH4
-// walks return the same (brute-force) answer.
+// Both results are independent of the visiting order, so every tree (host
+// SAH, device LBVH / PLOC) returns the same (brute-force) answer.
 constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 
 template <int STACK>
@@ -493,104 +449,15 @@ __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
   return n;
 }
 
-// Quantised BVH4 (width code 5, mrt_layout.h): the node's four rows, from LDS
-// for staged top nodes, else global memory.
-template <int MODE>
-__device__ __forceinline__ void fetch_node4q(const DeviceScene& sc, const LdsCtx& cx, int32_t node, float4 q[4]) {
-  if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = g_lds[4 * node + i];
-  } else {
-    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 4 * (size_t)node;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = p[i];
-  }
-}
-
-// slab entry distance of quantised plane q on one axis (BVH8 and quantised
-// BVH4): precise ((p + 2^e q) - o) * inv, the plane exactly as the builder
-// checked it; fast fma(q, 2^e inv, (p - o) inv)
-struct Axis8 { float p, s, o, inv, sinv, base; };
-__device__ __forceinline__ float qslab(float qf, const Axis8& a) {
-#if MRT_PRECISE
-  return ((a.p + a.s * qf) - a.o) * a.inv;
-#else
-  return fmaf(qf, a.sinv, a.base);
-#endif
-}
-__device__ __forceinline__ void q_axes(const float4& q0, V3 o, const RayBox& rb, Axis8 ax[3]) {
-  const uint32_t ew = fbits(q0.w);
-  const float pp[3] = {q0.x, q0.y, q0.z}, oo[3] = {o.x, o.y, o.z}, iv[3] = {rb.inv.x, rb.inv.y, rb.inv.z};
-#if !MRT_PRECISE
-  const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
-#endif
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    ax[a].p = pp[a];
-    ax[a].o = oo[a];
-    ax[a].inv = iv[a];
-    ax[a].s = bitsf((((ew >> (8 * a)) & 0xFFu) - 1u) << 23);   // 2^(byte - 128)
-#if !MRT_PRECISE
-    ax[a].sinv = ax[a].s * iv[a];
-    ax[a].base = fmaf(pp[a], iv[a], -oi[a]);
-#endif
-  }
-}
-
-// Box test of the four children of a quantised BVH4 node: entry distances,
-// +inf for a miss or an empty slot.  The near plane of each axis is the hi
-// byte where the direction is negative (slab distances are monotone in the
-// plane), so no planes are paired by min/max.
-__device__ __forceinline__ void box4q(const float4* q, V3 o, const RayBox& rb, float tmin, float tmax, float tn[4]) {
-  Axis8 ax[3];
-  q_axes(q[0], o, rb, ax);
-  const uint32_t sx = fbits(rb.inv.x) >> 31, sy = fbits(rb.inv.y) >> 31, sz = fbits(rb.inv.z) >> 31;
-  const uint32_t lx = fbits(q[2].x), hx = fbits(q[2].y), ly = fbits(q[2].z), hy = fbits(q[2].w);
-  const uint32_t lz = fbits(q[3].x), hz = fbits(q[3].y);
-  const uint32_t nx = sx ? hx : lx, fx = sx ? lx : hx, ny = sy ? hy : ly, fy = sy ? ly : hy;
-  const uint32_t nz = sz ? hz : lz, fz = sz ? lz : hz;
-  const uint32_t ref[4] = {fbits(q[1].x), fbits(q[1].y), fbits(q[1].z), fbits(q[1].w)};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int sh = 8 * k;
-    const float tnx = qslab((float)((nx >> sh) & 0xFFu), ax[0]), tfx = qslab((float)((fx >> sh) & 0xFFu), ax[0]);
-    const float tny = qslab((float)((ny >> sh) & 0xFFu), ax[1]), tfy = qslab((float)((fy >> sh) & 0xFFu), ax[1]);
-    const float tnz = qslab((float)((nz >> sh) & 0xFFu), ax[2]), tfz = qslab((float)((fz >> sh) & 0xFFu), ax[2]);
-    const float tnear = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-    const float tfar = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
-    const bool live = (int32_t)ref[k] != kEmptyChild;
-    tn[k] = (live & (tnear <= tfar)) ? tnear : __builtin_inff();
-  }
-}
-
 // One interior node: returns the next node to visit (nearest hit child, or a
 // popped entry, or kDone); the other hit children are pushed far-to-near.
-template <int STACK, int MODE, int WIDTH, bool ANY>
+template <int STACK, int MODE, bool ANY>
 __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const LdsCtx& cx, int32_t node, V3 o,
                                                  const RayBox& rb, float tmin, float tmax, int& sp) {
-  if constexpr (WIDTH == 2) {
-    float4 a, b, c, e;
-    fetch_node<MODE>(sc, cx, node, a, b, c, e);
-    bool hl, hr;
-    float tnl, tnr;
-    box2(a, b, c, o, rb, tmin, tmax, hl, hr, tnl, tnr);
-    const int32_t rl = (int32_t)fbits(e.x), rr = (int32_t)fbits(e.y);
-    if (!(hl | hr)) return stack_pop<STACK>(cx, sp);
-    const bool right_first = !hl || (hr && tnr < tnl);
-    if (hl & hr) {
-      stack_push<STACK>(cx, sp, right_first ? rl : rr);
-      ++sp;
-    }
-    return right_first ? rr : rl;
-  } else {
+  {
     float t[4];
     int32_t r[4];
-    if constexpr (WIDTH == 5) {   // quantised BVH4: one 64-B line per node
-      float4 q[4];
-      fetch_node4q<MODE>(sc, cx, node, q);
-      box4q(q, o, rb, tmin, tmax, t);
-      r[0] = (int32_t)fbits(q[1].x); r[1] = (int32_t)fbits(q[1].y); r[2] = (int32_t)fbits(q[1].z); r[3] = (int32_t)fbits(q[1].w);
-    } else {
+    {
       float4 q[7];
       fetch_node4<MODE>(sc, cx, node, rb, q);
       box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0)>(q, o, rb, tmin, tmax, t);
@@ -664,7 +531,7 @@ __device__ __forceinline__ bool leaf_tests(const DeviceScene& sc, const LdsCtx& 
   return false;
 }
 
-template <int STACK, int MODE, int WIDTH, bool ANY>
+template <int STACK, int MODE, bool ANY>
 __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
                                          uint32_t target) {
   const RayBox rb = make_raybox(o, d);
@@ -674,7 +541,7 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
   while (node != kDone || leaf != 0) {
     // interior nodes
     while (node != kDone && node >= 0) {
-      node = interior_step<STACK, MODE, WIDTH, ANY>(sc, cx, node, o, rb, tmin, h.t, sp);
+      node = interior_step<STACK, MODE, ANY>(sc, cx, node, o, rb, tmin, h.t, sp);
       if (node < 0 && leaf == 0) {   // park the leaf, keep descending
         leaf = node;
         node = stack_pop<STACK>(cx, sp);
@@ -697,162 +564,7 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
 }
 
 
-// ---------------------------------------------------------------------------
-// Compressed BVH8 traversal (node layout in mrt_layout.h), for scenes whose
-// nodes live in global memory (top levels staged in LDS).  Stack entries are
-// groups, two words each ([entry][lane] planes in LDS, spilling to global):
-//   node group     (base node, pending children in visiting order | imask << 8)
-//   triangle group (first triangle, pending triangle bits | 1 << 31)
-// A lane descends interior nodes while it holds at most one parked triangle
-// group (postponing, as in the BVH4 walk) until every lane of the wave holds
-// one; then the wave tests triangles.  Child visiting order: slot (k ^ ray
-// octant) k-th, no sorting.  Nearest / any-hit answers are order independent.
-// ---------------------------------------------------------------------------
-template <int STACK>
-__device__ __forceinline__ void stack_push2(const LdsCtx& cx, int sp, uint32_t lo, uint32_t hi) {
-  constexpr int kL = STACK < 0 ? -STACK : STACK;
-  if (STACK > 0 || sp < kL) {
-    lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock] = lo;
-    lds_u32()[cx.stack_base + threadIdx.x + (kL + sp) * kBlock] = hi;
-  } else {
-    cx.spill[spill_index(cx, 2 * (sp - kL))] = lo;
-    cx.spill[spill_index(cx, 2 * (sp - kL)) + 1] = hi;
-  }
-}
-template <int STACK>
-__device__ __forceinline__ void stack_get2(const LdsCtx& cx, int sp, uint32_t& lo, uint32_t& hi) {
-  constexpr int kL = STACK < 0 ? -STACK : STACK;
-  if (STACK > 0 || sp < kL) {
-    lo = lds_u32()[cx.stack_base + threadIdx.x + sp * kBlock];
-    hi = lds_u32()[cx.stack_base + threadIdx.x + (kL + sp) * kBlock];
-  } else {
-    lo = cx.spill[spill_index(cx, 2 * (sp - kL))];
-    hi = cx.spill[spill_index(cx, 2 * (sp - kL)) + 1];
-  }
-}
-
-template <int MODE>
-__device__ __forceinline__ void fetch_node8(const DeviceScene& sc, const LdsCtx& cx, uint32_t node, float4 q[5]) {
-  if (MODE == kAllLds || (MODE == kTopLds && node < cx.n_lds_nodes)) {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) q[i] = g_lds[5 * node + i];
-  } else {
-    const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 5 * (size_t)node;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) q[i] = p[i];
-  }
-}
-
-// permute the 8 slot bits of x so bit (s ^ oct) holds slot s
-__device__ __forceinline__ uint32_t octant_order(uint32_t x, uint32_t oct) {
-  x = (oct & 1u) ? (((x & 0x55u) << 1) | ((x >> 1) & 0x55u)) : x;
-  x = (oct & 2u) ? (((x & 0x33u) << 2) | ((x >> 2) & 0x33u)) : x;
-  x = (oct & 4u) ? (((x & 0x0Fu) << 4) | ((x >> 4) & 0x0Fu)) : x;
-  return x;
-}
-
-
-// Test the 8 children of a node: returns the hit slot mask; tri_bits gets the
-// triangle bits of the hit leaf slots (relative to the node's tri_base).
-__device__ __forceinline__ uint32_t box8(const float4 q[5], V3 o, const RayBox& rb, float tmin, float tmax,
-                                         uint32_t& tri_bits) {
-  Axis8 ax[3];
-  q_axes(q[0], o, rb, ax);
-  // near / far byte planes by the direction's signs (inv < 0: the hi plane is near)
-  const uint32_t sx = fbits(rb.inv.x) >> 31, sy = fbits(rb.inv.y) >> 31, sz = fbits(rb.inv.z) >> 31;
-  const uint32_t lx0 = fbits(q[2].x), lx1 = fbits(q[2].y), ly0 = fbits(q[2].z), ly1 = fbits(q[2].w);
-  const uint32_t lz0 = fbits(q[3].x), lz1 = fbits(q[3].y), hx0 = fbits(q[3].z), hx1 = fbits(q[3].w);
-  const uint32_t hy0 = fbits(q[4].x), hy1 = fbits(q[4].y), hz0 = fbits(q[4].z), hz1 = fbits(q[4].w);
-  const uint32_t nx[2] = {sx ? hx0 : lx0, sx ? hx1 : lx1}, fx[2] = {sx ? lx0 : hx0, sx ? lx1 : hx1};
-  const uint32_t ny[2] = {sy ? hy0 : ly0, sy ? hy1 : ly1}, fy[2] = {sy ? ly0 : hy0, sy ? ly1 : hy1};
-  const uint32_t nz[2] = {sz ? hz0 : lz0, sz ? hz1 : lz1}, fz[2] = {sz ? lz0 : hz0, sz ? lz1 : hz1};
-  const uint32_t meta[2] = {fbits(q[1].z), fbits(q[1].w)};
-  uint32_t hits = 0, tb = 0;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int w = c >> 2, sh = 8 * (c & 3);
-    const float tnx = qslab((float)((nx[w] >> sh) & 0xFFu), ax[0]), tfx = qslab((float)((fx[w] >> sh) & 0xFFu), ax[0]);
-    const float tny = qslab((float)((ny[w] >> sh) & 0xFFu), ax[1]), tfy = qslab((float)((fy[w] >> sh) & 0xFFu), ax[1]);
-    const float tnz = qslab((float)((nz[w] >> sh) & 0xFFu), ax[2]), tfz = qslab((float)((fz[w] >> sh) & 0xFFu), ax[2]);
-    const float tnear = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-    const float tfar = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
-    const bool hit = tnear <= tfar;
-    const uint32_t m = (meta[w] >> sh) & 0xFFu;
-    hits |= hit ? (1u << c) : 0u;
-    tb |= hit ? ((m >> 5) << (m & 31u)) : 0u;
-  }
-  tri_bits = tb;
-  return hits;
-}
-
-template <int STACK, int MODE, bool ANY>
-__device__ __forceinline__ bool traverse8(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
-                                          uint32_t target) {
-  const RayBox rb = make_raybox(o, d);
-  const uint32_t oct = (fbits(rb.inv.x) >> 31) | ((fbits(rb.inv.y) >> 31) << 1) | ((fbits(rb.inv.z) >> 31) << 2);
-  uint32_t gbase = (uint32_t)sc.root, gbits = 1u;   // the root: one pending child at rank 0 (imask 0)
-  uint32_t tbase = 0, tbits = 0;                    // parked triangle group
-  int sp = 0;
-  while ((gbits & 0xFFu) | tbits | (uint32_t)sp) {
-    // interior nodes
-    for (;;) {
-      if ((gbits & 0xFFu) == 0) {
-        if (sp == 0) break;
-        uint32_t lo, hi;
-        stack_get2<STACK>(cx, sp - 1, lo, hi);
-        if (hi >> 31) {                 // a postponed triangle group
-          if (tbits) break;             //   one is parked already: test that first
-          tbase = lo;
-          tbits = hi & 0x00FFFFFFu;
-          --sp;
-          break;
-        }
-        gbase = lo;
-        gbits = hi;
-        --sp;
-      }
-      const uint32_t k = __builtin_ctz(gbits & 0xFFu);
-      gbits &= gbits - 1u;              // the low byte is non-zero: clears bit k
-      const uint32_t slot = k ^ oct;
-      const uint32_t node = gbase + __popc((gbits >> 8) & ((1u << slot) - 1u));
-      if (gbits & 0xFFu) { stack_push2<STACK>(cx, sp, gbase, gbits); ++sp; }
-      float4 q[5];
-      fetch_node8<MODE>(sc, cx, node, q);
-      uint32_t tb;
-      const uint32_t hitm = box8(q, o, rb, tmin, h.t, tb);
-      const uint32_t imask = fbits(q[0].w) >> 24;
-      gbase = fbits(q[1].x);
-      gbits = octant_order(hitm & imask, oct) | (imask << 8);
-      if (tb) {
-        if (tbits) { stack_push2<STACK>(cx, sp, fbits(q[1].y), tb | 0x80000000u); ++sp; }
-        else { tbase = fbits(q[1].y); tbits = tb; }
-      }
-      if (!__any(tbits == 0)) break;    // every lane still descending holds triangles
-    }
-    // triangles of the parked group
-    while (tbits) {
-      const uint32_t k = __builtin_ctz(tbits);
-      tbits &= tbits - 1u;
-      float4 t0, t1, t2;
-      fetch_tri<MODE>(sc, cx, tbase + k, t0, t1, t2);
-      const uint32_t prim = fbits(t0.w);
-      float t, u, v;
-      const bool hit = tri_test(o, d, mk(t0), mk(t1), mk(t2), tmin, h.t, t, u, v);
-      if (ANY) {
-        if (hit & (prim != target) & ((t < h.t) | (prim < target))) return true;
-      } else if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
-        h.found = true;
-        h.t = t;
-        h.u = u;
-        h.v = v;
-        h.prim = prim;
-      }
-    }
-  }
-  return false;
-}
-
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
                                              float tmax) {
   Hit h;
@@ -860,32 +572,30 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
-  if constexpr (WIDTH == 8) traverse8<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u);
-  else traverse<STACK, MODE, WIDTH, false>(sc, cx, o, d, tmin, h, 0u);
+  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u);
   return h;
 }
 
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
                                                float t_target) {
   Hit h;
   h.t = t_target;
   h.found = false;
-  if constexpr (WIDTH == 8) return traverse8<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target);
-  else return traverse<STACK, MODE, WIDTH, true>(sc, cx, o, d, 0.0f, h, target);
+  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target);
 }
 
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
 // (renderer/Shaders.metal:214-231): contributes iff the nearest hit of the
 // shadow ray (tmin 0, tmax inf) is the target triangle at t >= 1e-4.
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target) {
   const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
   float tT, u, v;
   if (!tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v)) return false;
   if (!(tT >= kDistanceEpsilon)) return false;
-  return !trace_occluded<STACK, MODE, WIDTH>(sc, cx, o, d, target, tT);
+  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT);
 }
 
 // ---------------------------------------------------------------------------
@@ -1316,7 +1026,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* v, uint32_t n
 // Used by bounce_kernel (one launch per bounce) and, with WAVEQ (the wave's
 // own queue: survivors at out_base + their rank among the wave's survivors,
 // no cursors, no class split), by stream_kernel.
-template <int STACK, int MODE, int WIDTH, bool WAVEQ = false>
+template <int STACK, int MODE, bool WAVEQ = false>
 __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const LdsCtx& cx, const BounceArgs& a,
                                                uint32_t bounce, bool active, uint32_t idx, uint32_t slot,
                                                const RayQueue& in_q, const RayQueue& out_q, uint32_t* cursor,
@@ -1355,7 +1065,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   // -- phase 1: nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
   Hit h;
   h.found = false;
-  if (active) h = trace_nearest<STACK, MODE, WIDTH>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+  if (active) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
   STAMP_AT(st, 1);
   // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
   //    near hit ends the path (:122-126)
@@ -1426,7 +1136,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   }
   STAMP_AT(st, 3);
   // -- phase 4: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
-  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE, WIDTH>(sc, cx, sh.o, sh.d, sh.target))) {
+  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target))) {
     s.R = add(s.R, sh.L);
   }
   if (alive && !(a.debug & 4u)) out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
@@ -1434,7 +1144,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   return wrote;
 }
 
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
   __shared__ uint32_t s_cursor[2], s_res, s_closed;
@@ -1538,7 +1248,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
                          : (lo - g_in) * in_chunk + in_chunk - (seg[lo + 1] - seg[lo]) + (idx - seg[lo]);
       }
       STAMP_BEGIN();
-      wrote += bounce_wave<STACK, MODE, WIDTH>(sc, cx, a, a.bounce, active, idx, slot, a.in_q, a.out_q, s_cursor,
+      wrote += bounce_wave<STACK, MODE>(sc, cx, a, a.bounce, active, idx, slot, a.in_q, a.out_q, s_cursor,
                                                out_base, cap, lanes_below, STAMP_REF());
     }
     STAMP_WORK();
@@ -1576,7 +1286,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
 // the camera rays are gone a wave runs its partial levels, deepest first.
 // No wave ever waits for another, so any grid and any residency is safe.
 // ---------------------------------------------------------------------------
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_cnt[kBlock / 64][kStreamMaxL];    // rays queued per level (wave-private rows)
   __shared__ uint32_t s_alive[kBlock / 64][kStreamMaxL];  // survivors per bounce (stats)
@@ -1651,7 +1361,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
     const uint32_t out = lvl + 1u < L ? qbase + lvl * kStreamCap + cnt[lvl + 1u] : 0u;
     // the wave reads rays its own lanes wrote: their stores first
     if (!camera) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t wrote = bounce_wave<STACK, MODE, WIDTH, true>(sc, cx, a, camera ? 0u : lvl, active, idx, slot,
+    const uint32_t wrote = bounce_wave<STACK, MODE, true>(sc, cx, a, camera ? 0u : lvl, active, idx, slot,
                                                                  a.in_q, a.in_q, nullptr, out, 0u, lanes_below, st);
     if (lvl + 1u < L && lane == 0) {
       cnt[lvl + 1u] += wrote;
@@ -1663,42 +1373,10 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
     if (s_alive[wave][b]) atomicAdd(a.bounce_counts + b, s_alive[wave][b]);
 }
 
-// ---------------------------------------------------------------------------
-// Lane-refill bounce kernel (global-memory scenes: kTopLds / kGlobal).
-//
-// In bounce_kernel a wave runs its 64 rays through nearest hit, shading and
-// the shadow query in lockstep, so every traversal phase lasts as long as its
-// slowest lane: on incoherent secondary rays over the 1M-triangle BVH the
-// SIMD efficiency of the traversal loop is ~0.3 (tools/bvh_stats.cpp).  Here
-// each lane carries a resumable traversal (node, parked leaf, stack) and the
-// wave runs traversal rounds until kRefillService lanes have finished their
-// query; the finished lanes are then serviced together — a finished nearest
-// query is shaded (MIS emission, next ray into the output queue, NEE shadow
-// ray that starts its occlusion query right away), a finished shadow query
-// adds its contribution and writes the ray's radiance plane — and idle lanes
-// take new rays from the wave's grab pool (persistent threads with dynamic
-// ray fetch, Aila & Laine 2009).  The arithmetic per ray is the same as in
-// bounce_kernel, so the image is identical (precise build: bitwise).
-// ---------------------------------------------------------------------------
-#ifndef MRT_REFILL_SERVICE
-#define MRT_REFILL_SERVICE 24
-#endif
-// 4 waves/SIMD: the resumable lane state keeps ~118 VGPRs live through the
-// shading of the finished lanes; at 5 waves (96 VGPRs) 85 of them spill and
-// C4 ran 10 % slower (tools/lib_sweep.sh, r2)
-#ifndef MRT_REFILL_WAVES
-#define MRT_REFILL_WAVES 4
-#endif
-
 struct Trav {
   int32_t node, leaf;
   int sp;
 };
-// words of lane state the refill kernel parks in LDS around a service phase
-// ([word][lane] after the traversal stack): ro, rd, h.t, h.u, h.v, h.prim,
-// tr.node, tr.leaf, tr.sp, aux0, aux1, flags
-constexpr uint32_t kLaneStateWords = 16;
-
 __device__ __forceinline__ void trav_begin(const DeviceScene& sc, Trav& tr) {
   tr.node = sc.root;
   tr.leaf = 0;
@@ -1713,12 +1391,12 @@ __device__ __forceinline__ bool trav_done(const Trav& tr) { return tr.node == kD
 // with (t_k, k) < (h.t, target) and sets `occluded`.
 // uv: when non-null, the nearest hit's barycentrics go to uv[0], uv[kBlock]
 // (the lane's LDS path state) instead of h.u, h.v.
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, const RayBox& rb,
                                            Hit& h, bool any, uint32_t target, bool& occluded, Trav& tr,
                                            uint32_t* uv = nullptr) {
   while (tr.node != kDone && tr.node >= 0) {
-    tr.node = interior_step<STACK, MODE, WIDTH, false>(sc, cx, tr.node, o, rb, 0.0f, h.t, tr.sp);
+    tr.node = interior_step<STACK, MODE, false>(sc, cx, tr.node, o, rb, 0.0f, h.t, tr.sp);
     if (tr.node < 0 && tr.leaf == 0) {
       tr.leaf = tr.node;
       tr.node = stack_pop<STACK>(cx, tr.sp);
@@ -1742,311 +1420,13 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
   }
 }
 
-template <int STACK, int MODE, int WIDTH>
-__global__ __launch_bounds__(kBlock, MRT_REFILL_WAVES) void bounce_refill_kernel(DeviceScene sc, BounceArgs a) {
-  __shared__ uint32_t s_wave[kBlock / 64];
-  __shared__ uint32_t s_cursor[4], s_res, s_closed;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t G = gridDim.x;
-  const uint32_t ncls = a.classes == 4u ? 4u : 2u;
-  const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
-  const LdsCtx cx = stage_lds<MODE>(sc, nseg + 1, a.stack_spill);
-  uint32_t* seg = lds_u32() + cx.scratch_base;
-  if (tid == 0) s_cursor[0] = s_cursor[1] = s_cursor[2] = s_cursor[3] = s_res = s_closed = 0;
-  uint32_t N, in_chunk = 0;
-  if (a.bounce == 0) {
-    N = a.num_slots * a.batch;
-    __syncthreads();
-  } else {
-    for (uint32_t i = tid; i < nseg; i += kBlock) seg[i] = a.in_seg_count[i];
-    __syncthreads();
-    N = block_exclusive_scan(seg, nseg, s_wave);
-    if (tid == 0) seg[nseg] = N;
-    __syncthreads();
-    in_chunk = *a.in_chunk;
-  }
-  const uint32_t chunk = ((N + G - 1) / G + kBlock - 1) / kBlock * kBlock;
-  // output reservation (see bounce_kernel): a wave reserves kGrab slots per
-  // grab; a ray holds one slot from the grab until it is shaded, when a
-  // survivor fills it and a finished path releases it (as do the grab's
-  // indices past its range and bounce-0 slots outside the image).  A wave
-  // thus holds at most kGrab (pool) + 64 (in flight) unfilled slots, 768 per
-  // block, below the slack kRefillSlack: a block that cannot reserve has
-  // written more than `chunk` survivors, so not every block can stop while
-  // input remains
-  const uint32_t cap = chunk + kRefillSlack;
-  const uint32_t out_base = blockIdx.x * (ncls >> 1) * cap;
-  const uint32_t rlen = ((N + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
-  uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
-  const uint32_t lane = tid & 63u;
-  const bool last = (a.bounce + 1 == a.max_path_length);
-  const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const uint32_t back = (a.bounce % 3u) == 0 ? 0u : ((a.bounce % 3u) == 1 ? 2u : 1u);
-  // this lane's parked-state words: after the traversal stack (kLaneStateWords x [word][lane])
-  const uint32_t st_base = cx.stack_base + threadIdx.x + (uint32_t)(STACK < 0 ? -STACK : STACK) * kBlock;
-
-  // wave-uniform pool of input indices [pool_next, pool_end) of the current grab
-  uint32_t pool_next = 0, pool_end = 0;
-  bool exhausted = false;
-  // lane state (registers are tight: everything a traversing lane keeps is
-  // live while other lanes shade, so the two queries share registers)
-  uint32_t phase = 0;                 // 0 idle, 1 nearest query, 2 shadow query
-  V3 ro = mk(0.0f, 0.0f, 0.0f), rd = mk(0.0f, 0.0f, 1.0f);
-  Trav tr{kDone, 0, 0};
-  Hit h;                              // nearest: the hit; shadow: h.t = t_target, (h.u, h.v, h.prim) = the
-  h.t = 0.0f; h.u = h.v = 0.0f;       //   light contribution L (x, y, bits of z)
-  h.prim = 0u; h.found = false;
-  bool occluded = false;
-  uint32_t aux0 = 0, aux1 = 0;        // nearest: (global slot | prevDiffuse << 31, input queue slot);
-                                      // shadow: (light triangle, output queue slot)
-
-  for (;;) {
-    // ---- refill idle lanes from the pool (grab when it runs dry)
-    for (;;) {
-      const uint64_t idle = __ballot(phase == 0);
-      if (!idle || exhausted) break;
-      if (pool_next >= pool_end) {
-        uint32_t got = 0xFFFFFFFFu;
-        if (lane == 0) {
-          if (atomicAdd(&s_res, kGrab) + kGrab <= cap) {
-            while (ranges_left) {
-              const uint32_t r0 = cur_range * rlen;
-              if (r0 < N && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
-                const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
-                if (i < rlen && r0 + i < N) { got = r0 + i; break; }
-                atomicOr(&s_closed, 1u << cur_range);
-              }
-              cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
-              --ranges_left;
-            }
-            if (got == 0xFFFFFFFFu) atomicSub(&s_res, kGrab);
-          } else {
-            got = 0xFFFFFFFEu;   // the block's output segment is full
-          }
-        }
-        got = __builtin_amdgcn_readfirstlane(got);
-        cur_range = __builtin_amdgcn_readfirstlane(cur_range);
-        ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
-        if (got >= 0xFFFFFFFEu) { exhausted = true; break; }
-        pool_next = got;
-        pool_end = min(N, min(got + kGrab, cur_range * rlen + rlen));
-        if (lane == 0 && pool_end - pool_next < kGrab) atomicSub(&s_res, kGrab - (pool_end - pool_next));
-      }
-      const uint32_t rank = (uint32_t)__popcll(idle & lanes_below);
-      const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool_next);
-      bool ok = true;
-      if (phase == 0 && rank < take) {
-        const uint32_t idx = pool_next + rank;
-        if (a.bounce == 0) {
-          const uint32_t fj = a.batch == 1u ? 0u : idx / a.num_slots;
-          uint32_t x, y;
-          slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
-          ok = (x < a.width) && (y < a.height);
-          if (ok) {
-            aux0 = idx;
-            const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
-            camera_ray(x, y, a.width, a.height, ns, ro, rd);
-          }
-        } else {
-          uint32_t lo = 0, hi = nseg;
-          while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (seg[mid] <= idx) lo = mid; else hi = mid; }
-          // segment lo = class c of block j: c even from the front of the
-          // block's (c >> 1)-th cap-slot segment, c odd from its back
-          const uint32_t g_in = nseg / ncls, c = lo / g_in, j = lo - c * g_in;
-          const uint32_t sbase = (j * (ncls >> 1) + (c >> 1)) * in_chunk;
-          aux1 = (c & 1u) ? sbase + in_chunk - (seg[lo + 1] - seg[lo]) + (idx - seg[lo]) : sbase + (idx - seg[lo]);
-          const float4 q0 = a.in_q.plane[0][aux1], q1 = a.in_q.plane[1][aux1];
-          ro = mk(q0);
-          aux0 = fbits(q0.w);
-          rd = mk(q1);
-        }
-        if (ok) {
-          phase = 1;
-          trav_begin(sc, tr);
-          h.t = __builtin_inff();
-          h.u = h.v = 0.0f;
-          h.prim = 0xFFFFFFFFu;
-          h.found = false;
-        }
-      }
-      const uint64_t bad = __ballot(!ok);   // bounce-0 slots outside the image release their output slot
-      if (lane == 0 && bad) atomicSub(&s_res, (uint32_t)__popcll(bad));
-      pool_next += take;
-    }
-    if (!__any(phase != 0)) break;   // every lane idle and no input left
-
-    // ---- traversal rounds until enough lanes have finished their query
-    bool fin = phase != 0 && trav_done(tr);
-    for (;;) {
-      const uint64_t going = __ballot(phase != 0 && !fin);
-      if (!going) break;
-      if ((uint32_t)__popcll(__ballot(fin)) >= (exhausted ? 1u : (uint32_t)MRT_REFILL_SERVICE)) break;
-      if (phase != 0 && !fin) {
-        const RayBox rb = make_raybox(ro, rd);   // recomputed per round: not live across shading
-        trav_round<STACK, MODE, WIDTH>(sc, cx, ro, rd, rb, h, phase == 2, aux0, occluded, tr);
-        fin = trav_done(tr);
-      }
-    }
-
-    if (!__any(fin)) continue;
-
-    // ---- service.  Every lane's state is parked in LDS first, so while the
-    //      finished lanes shade, the traversing lanes' registers are free
-    //      (the live set of the shading code alone fits the register budget)
-    uint32_t* const ls = lds_u32() + st_base;
-    ls[0 * kBlock] = fbits(ro.x); ls[1 * kBlock] = fbits(ro.y); ls[2 * kBlock] = fbits(ro.z);
-    ls[3 * kBlock] = fbits(rd.x); ls[4 * kBlock] = fbits(rd.y); ls[5 * kBlock] = fbits(rd.z);
-    ls[6 * kBlock] = fbits(h.t); ls[7 * kBlock] = fbits(h.u); ls[8 * kBlock] = fbits(h.v); ls[9 * kBlock] = h.prim;
-    ls[10 * kBlock] = (uint32_t)tr.node; ls[11 * kBlock] = (uint32_t)tr.leaf; ls[12 * kBlock] = (uint32_t)tr.sp;
-    ls[13 * kBlock] = aux0; ls[14 * kBlock] = aux1;
-    ls[15 * kBlock] = phase | (h.found ? 4u : 0u) | (occluded ? 8u : 0u) | (fin ? 16u : 0u);
-    {
-      const uint32_t flags = ls[15 * kBlock];
-      const uint32_t ph = flags & 3u;
-      const bool done = (flags & 16u) != 0;
-      // finished shadow queries (MPS nearest-hit semantics + lightSamplingHandler,
-      // Shaders.metal:214-231): the ray's radiance plane was written without
-      // the light; add it when the target is visible
-      if (done && ph == 2) {
-        const uint32_t os = ls[14 * kBlock];
-        if (!(flags & 8u)) {
-          const float4 q3 = a.out_q.plane[3][os];
-          a.out_q.plane[3][os] = make_float4(q3.x + bitsf(ls[7 * kBlock]), q3.y + bitsf(ls[8 * kBlock]),
-                                             q3.z + bitsf(ls[9 * kBlock]), q3.w);
-        }
-        ls[15 * kBlock] = 0u;
-      }
-      // finished nearest queries (intersectionHandler, Shaders.metal:105-212)
-      const bool shade_now = done && ph == 1;
-      PathState s;
-      ShadowRay sh;
-      sh.valid = false;
-      bool hit_ok = false;
-      uint32_t gslot = 0, tagv = 0;
-      Hit hh;
-      if (shade_now) {
-        s.o = mk(bitsf(ls[0 * kBlock]), bitsf(ls[1 * kBlock]), bitsf(ls[2 * kBlock]));
-        s.d = mk(bitsf(ls[3 * kBlock]), bitsf(ls[4 * kBlock]), bitsf(ls[5 * kBlock]));
-        hh.t = bitsf(ls[6 * kBlock]); hh.u = bitsf(ls[7 * kBlock]); hh.v = bitsf(ls[8 * kBlock]);
-        hh.prim = ls[9 * kBlock]; hh.found = (flags & 4u) != 0;
-        tagv = ls[13 * kBlock];
-        s.prevDiffuse = (tagv >> 31) ? 1.0f : 0.0f;
-        gslot = tagv & 0x7FFFFFFFu;
-        if (a.bounce == 0) {
-          s.T = mk(1.0f, 1.0f, 1.0f);
-          s.R = mk(0.0f, 0.0f, 0.0f);
-          s.pdf = 1.0f;
-          s.prevDiffuse = 0.0f;
-          s.ior = 1.00029f;
-        } else {
-          const uint32_t is = ls[14 * kBlock];
-          const float4 q2 = a.in_q.plane[2][is], q3 = a.in_q.plane[3][is];
-          s.T = mk(q2);
-          s.pdf = q2.w;
-          s.R = mk(q3);
-          s.ior = q3.w;
-        }
-        hit_ok = hh.found && !(hh.t < kDistanceEpsilon);
-        if (hit_ok) {
-          const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;
-          uint32_t x, y;
-          slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
-          const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, a.bounce, a.frame_index + fj)];
-          shade_hit<MODE>(sc, cx, hh, s, ns, a.bounce, a.max_path_length, !last, sh);
-        }
-        if (!hit_ok || last) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
-      }
-      // survivors -> this block's segment of the next queue (material classes)
-      const bool alive = shade_now && hit_ok && !last;
-      // class: 2 classes = left a diffuse surface or not; 4 = the material
-      // type left (MRT_DEBUG bit 16: everything in class 0)
-      const uint32_t cls = (a.debug & 16u) ? 0u : ncls == 4u ? s.mtype : (s.prevDiffuse == 0.0f ? 1u : 0u);
-      uint64_t mask[4];
-#pragma unroll
-      for (uint32_t c = 0; c < 4; ++c) mask[c] = (c < ncls) ? __ballot(alive && cls == c) : 0ull;
-      uint32_t oslot = 0;
-      if (mask[0] | mask[1] | mask[2] | mask[3]) {
-        uint32_t w[4] = {0, 0, 0, 0};
-        if (lane == 0) {
-#pragma unroll
-          for (uint32_t c = 0; c < 4; ++c)
-            if (mask[c]) w[c] = atomicAdd(&s_cursor[c], (uint32_t)__popcll(mask[c]));
-        }
-        uint32_t mine = 0, before = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < 4; ++c) {
-          const uint32_t wc = __shfl(w[c], 0);
-          if (cls == c) { mine = wc; before = (uint32_t)__popcll(mask[c] & lanes_below); }
-        }
-        if (alive) {
-          const uint32_t sb = out_base + (cls >> 1) * cap;
-          oslot = (cls & 1u) ? sb + cap - 1u - (mine + before) : sb + mine + before;
-          a.out_q.plane[0][oslot] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
-          a.out_q.plane[1][oslot] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
-          a.out_q.plane[2][oslot] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
-          a.out_q.plane[3][oslot] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
-        }
-      }
-      const uint64_t ended = __ballot(shade_now && !alive);   // finished paths release their output slot
-      if (lane == 0 && ended) atomicSub(&s_res, (uint32_t)__popcll(ended));
-      if (shade_now) {
-        uint32_t nflags = 0u;
-        if (alive && sh.valid) {
-          // the shadow ray: MPS nearest hit == target test + occlusion query
-          // (shadow_reaches_target); the query runs in the next rounds
-          const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
-          const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
-          float tT, u, v;
-          if (tri_test(sh.o, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
-              !(tT < kDistanceEpsilon)) {
-            Trav t0;
-            trav_begin(sc, t0);
-            ls[0 * kBlock] = fbits(sh.o.x); ls[1 * kBlock] = fbits(sh.o.y); ls[2 * kBlock] = fbits(sh.o.z);
-            ls[3 * kBlock] = fbits(sh.d.x); ls[4 * kBlock] = fbits(sh.d.y); ls[5 * kBlock] = fbits(sh.d.z);
-            ls[6 * kBlock] = fbits(tT);
-            ls[7 * kBlock] = fbits(sh.L.x); ls[8 * kBlock] = fbits(sh.L.y); ls[9 * kBlock] = fbits(sh.L.z);
-            ls[10 * kBlock] = (uint32_t)t0.node; ls[11 * kBlock] = (uint32_t)t0.leaf; ls[12 * kBlock] = 0u;
-            ls[13 * kBlock] = sh.target;
-            ls[14 * kBlock] = oslot;
-            nflags = 2u;
-          }
-        }
-        ls[15 * kBlock] = nflags;
-      }
-    }
-    // ---- every lane resumes from its parked (or new) state
-    ro = mk(bitsf(ls[0 * kBlock]), bitsf(ls[1 * kBlock]), bitsf(ls[2 * kBlock]));
-    rd = mk(bitsf(ls[3 * kBlock]), bitsf(ls[4 * kBlock]), bitsf(ls[5 * kBlock]));
-    h.t = bitsf(ls[6 * kBlock]); h.u = bitsf(ls[7 * kBlock]); h.v = bitsf(ls[8 * kBlock]); h.prim = ls[9 * kBlock];
-    tr.node = (int32_t)ls[10 * kBlock]; tr.leaf = (int32_t)ls[11 * kBlock]; tr.sp = (int)ls[12 * kBlock];
-    aux0 = ls[13 * kBlock]; aux1 = ls[14 * kBlock];
-    {
-      const uint32_t flags = ls[15 * kBlock];
-      phase = flags & 3u;
-      h.found = (flags & 4u) != 0;
-      occluded = (flags & 8u) != 0;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t total = 0;
-    for (uint32_t c = 0; c < ncls; ++c) {
-      a.out_seg_count[c * G + blockIdx.x] = s_cursor[c];
-      total += s_cursor[c];
-    }
-    if (total) atomicAdd(a.out_total, total);
-    if (blockIdx.x == 0) *a.out_chunk = cap;
-  }
-}
-
-
 // ---------------------------------------------------------------------------
 // Path megakernel: all MAX_PATH_LENGTH bounces of a batch of frames in ONE
 // launch.  Each lane carries a whole path — camera ray, then per bounce the
 // nearest-hit query, intersectionHandler, the NEE shadow query and
 // lightSamplingHandler, in the reference's order (renderer/Renderer.mm:
 // 500-585) — as a sequence of resumable traversal queries (trav_round); when
-// kRefillService lanes have finished their query the wave services them
+// MRT_PATH_SERVICE lanes have finished their query the wave services them
 // together (shading or the shadow resolve, then the next query of the same
 // path), and a lane whose path ended takes the next pixel sample from the
 // wave's grab pool.  Compared with the wavefront of per-bounce launches there
@@ -2066,7 +1446,7 @@ constexpr uint32_t kPathStateWords = 16;
 #define MRT_PATH_SERVICE 24
 #endif
 
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_closed;
   __shared__ uint32_t s_count[64];   // rays alive at the start of bounce b + 1 (stats)
@@ -2152,7 +1532,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       if ((uint32_t)__popcll(__ballot(fin)) >= (exhausted ? 1u : (uint32_t)MRT_PATH_SERVICE)) break;
       if (phase != 0 && !fin) {
         const RayBox rb = make_raybox(ro, rd);
-        trav_round<STACK, MODE, WIDTH>(sc, cx, ro, rd, rb, h, phase == 2, target, occluded, tr);
+        trav_round<STACK, MODE>(sc, cx, ro, rd, rb, h, phase == 2, target, occluded, tr);
         fin = trav_done(tr);
       }
     }
@@ -2291,7 +1671,7 @@ __global__ __launch_bounds__(kBlock) void raygen_kernel(uint32_t W, uint32_t H, 
   for (int k = 0; k < 3; ++k) { r.throughput[k] = 1.0f; r.radiance[k] = 0.0f; }
 }
 
-template <int WIDTH, int STACK>
+template <int STACK>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DeviceScene sc, const uint8_t* rays, uint32_t stride,
                                                            uint32_t count, RefIntersection* out, uint32_t* spill) {
   const LdsCtx cx = stage_lds<kGlobal>(sc, 0, spill);
@@ -2301,7 +1681,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DeviceScene sc, const
     const float tmax = r[7];
     if (tmax >= 0.0f) {   // maxDistance < 0 disables the ray (Shaders.metal:124,173)
       const V3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
-      const Hit h = trace_nearest<STACK, kGlobal, WIDTH>(sc, cx, o, d, r[3], tmax);
+      const Hit h = trace_nearest<STACK, kGlobal>(sc, cx, o, d, r[3], tmax);
       if (h.found) {
         res.distance = h.t;
         res.triangleIndex = h.prim;
@@ -2387,14 +1767,11 @@ int choose_mode(const DeviceScene& sc) {
   return sc.lds_nodes > 0 ? kTopLds : kGlobal;
 }
 
-size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid, bool refill) {
+size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
   const size_t scene = (size_t)lds_scene_float4s(mode, node_float4s(sc.width), sc.num_nodes, sc.lds_nodes,
                                                  sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16;
-  // segment counts per block (2 classes; the lane-refill kernel reserves 4) + sentinel
-  const size_t scratch = ((size_t)(refill ? 4 : 2) * grid + 1 + 3) / 4 * 16;
-  const size_t entry_words = sc.width == 8 ? 2 : 1;              // BVH8: two-word group entries
-  const size_t lane_state = refill ? (size_t)kLaneStateWords * kBlock * 4 : 0;   // lane-refill kernel
-  return scene + scratch + (size_t)stack * entry_words * kBlock * 4 + lane_state;   // stack = LDS entries (|STACK|)
+  const size_t scratch = ((size_t)2 * grid + 1 + 3) / 4 * 16;   // segment counts per block (2 classes) + sentinel
+  return scene + scratch + (size_t)stack * kBlock * 4;           // stack = LDS entries (|STACK|)
 }
 
 // kTopLds: stage only as many top BVH nodes as keep the block's LDS within
@@ -2406,36 +1783,18 @@ size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_
 #ifndef MRT_LDS_BLOCKS
 #define MRT_LDS_BLOCKS MRT_BOUNCE_WAVES
 #endif
-#ifndef MRT_REFILL_LDS_BLOCKS
-#define MRT_REFILL_LDS_BLOCKS 4   // the lane-refill kernel's resident blocks per CU (MRT_REFILL_WAVES)
-#endif
-bool refill_enabled();
 DeviceScene fit_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
   if (mode != kTopLds) return sc;
   DeviceScene f = sc;
-  const bool refill = sc.width != 8 && refill_enabled();
-  const size_t blocks = refill ? MRT_REFILL_LDS_BLOCKS : MRT_LDS_BLOCKS;
-  const size_t kLdsPerBlockTarget = 160 * 1024 / blocks - 2048;
-  const size_t fixed = bounce_lds_bytes(sc, kGlobal, stack, grid, refill) + 64;   // scratch + stack + lane state + static
+  const size_t kLdsPerBlockTarget = 160 * 1024 / MRT_LDS_BLOCKS - 2048;
+  const size_t fixed = bounce_lds_bytes(sc, kGlobal, stack, grid) + 64;   // scratch + stack + static
   const size_t node_bytes = (size_t)node_float4s(sc.width) * 16;
   const size_t fit = fixed < kLdsPerBlockTarget ? (kLdsPerBlockTarget - fixed) / node_bytes : 0;
   f.lds_nodes = (uint32_t)std::min<size_t>(sc.lds_nodes, fit);
   return f;
 }
 
-// the lane-refill kernel serves the global-memory modes (MRT_REFILL=0 keeps
-// bounce_kernel there, for A/B measurements)
-bool refill_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("MRT_REFILL");
-    return !v || std::atoi(v) != 0;
-  }();
-  return on;
-}
-template <int MODE, int WIDTH>
-bool use_refill() { return MODE != kAllLds && WIDTH != 8 && refill_enabled(); }
-
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* grid) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -2451,11 +1810,9 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* gri
   int n = 1;
   for (int want = 8; want >= 1; --want) {
     const uint32_t g = cus * (uint32_t)want;
-    const size_t lds = bounce_lds_bytes(fit_lds_nodes(sc, MODE, stack, g), MODE, stack, g, use_refill<MODE, WIDTH>());
+    const size_t lds = bounce_lds_bytes(fit_lds_nodes(sc, MODE, stack, g), MODE, stack, g);
     int occ = 0;
-    const void* fn = use_refill<MODE, WIDTH>() ? (const void*)bounce_refill_kernel<STACK, MODE, WIDTH>
-                                               : (const void*)bounce_kernel<STACK, MODE, WIDTH>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBlock, lds) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bounce_kernel<STACK, MODE>, kBlock, lds) != hipSuccess)
       occ = 0;
     if (occ >= want) { n = want; break; }
   }
@@ -2483,7 +1840,7 @@ DeviceScene fit_path_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack) 
   return f;
 }
 
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 hipError_t path_grid_t(const DeviceScene& sc, uint32_t* grid) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -2494,119 +1851,96 @@ hipError_t path_grid_t(const DeviceScene& sc, uint32_t* grid) {
   const int stack = STACK < 0 ? -STACK : STACK;
   const size_t lds = path_lds_bytes(fit_path_lds_nodes(sc, MODE, stack), MODE, stack);
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, path_kernel<STACK, MODE, WIDTH>, kBlock, lds) != hipSuccess || occ < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, path_kernel<STACK, MODE>, kBlock, lds) != hipSuccess || occ < 1)
     occ = 1;
   *grid = (uint32_t)prop.multiProcessorCount * (uint32_t)std::min(occ, 8);
   return hipSuccess;
 }
 
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 hipError_t launch_path_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
   const int stack = STACK < 0 ? -STACK : STACK;
   const DeviceScene f = fit_path_lds_nodes(sc, MODE, stack);
-  path_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), path_lds_bytes(f, MODE, stack), s>>>(f, a);
+  path_kernel<STACK, MODE><<<dim3(grid), dim3(kBlock), path_lds_bytes(f, MODE, stack), s>>>(f, a);
   return hipGetLastError();
 }
 
-template <int STACK, int WIDTH>
+template <int STACK>
 hipError_t path_dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
                               hipStream_t s) {
   switch (choose_mode(sc)) {
     case kAllLds:
-      return a ? launch_path_t<STACK, kAllLds, WIDTH>(sc, *a, grid, s) : path_grid_t<STACK, kAllLds, WIDTH>(sc, grid_out);
+      return a ? launch_path_t<STACK, kAllLds>(sc, *a, grid, s) : path_grid_t<STACK, kAllLds>(sc, grid_out);
     case kTopLds:
-      return a ? launch_path_t<STACK, kTopLds, WIDTH>(sc, *a, grid, s) : path_grid_t<STACK, kTopLds, WIDTH>(sc, grid_out);
+      return a ? launch_path_t<STACK, kTopLds>(sc, *a, grid, s) : path_grid_t<STACK, kTopLds>(sc, grid_out);
     default:
-      return a ? launch_path_t<STACK, kGlobal, WIDTH>(sc, *a, grid, s) : path_grid_t<STACK, kGlobal, WIDTH>(sc, grid_out);
+      return a ? launch_path_t<STACK, kGlobal>(sc, *a, grid, s) : path_grid_t<STACK, kGlobal>(sc, grid_out);
   }
 }
 
-template <int STACK>
-hipError_t path_dispatch_width(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
-                               hipStream_t s) {
-  return sc.width == 5   ? path_dispatch_mode<STACK, 5>(sc, a, grid, grid_out, s)
-         : sc.width == 4 ? path_dispatch_mode<STACK, 4>(sc, a, grid, grid_out, s)
-                         : path_dispatch_mode<STACK, 2>(sc, a, grid, grid_out, s);
-}
-
-// stack variants as for the bounce kernel; BVH8 scenes are not served here
+// LDS stack capacity variants (negative: |STACK| LDS entries + global spill)
 hipError_t path_dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_entries, uint32_t grid,
                          uint32_t* grid_out, hipStream_t s) {
-  if (sc.width == 8) return hipErrorInvalidValue;
+  if (sc.width != 4) return hipErrorInvalidValue;
   if (sc.max_stack > stack_entries) {
-    if (stack_entries <= 8) return path_dispatch_width<-8>(sc, a, grid, grid_out, s);
-    if (stack_entries <= 12) return path_dispatch_width<-12>(sc, a, grid, grid_out, s);
-    if (stack_entries <= 16) return path_dispatch_width<-16>(sc, a, grid, grid_out, s);
-    return path_dispatch_width<-32>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 8) return path_dispatch_mode<-8>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 12) return path_dispatch_mode<-12>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 16) return path_dispatch_mode<-16>(sc, a, grid, grid_out, s);
+    return path_dispatch_mode<-32>(sc, a, grid, grid_out, s);
   }
-  if (stack_entries <= 8) return path_dispatch_width<8>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 12) return path_dispatch_width<12>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 16) return path_dispatch_width<16>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 24) return path_dispatch_width<24>(sc, a, grid, grid_out, s);
-  return path_dispatch_width<32>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 8) return path_dispatch_mode<8>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 12) return path_dispatch_mode<12>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 16) return path_dispatch_mode<16>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 24) return path_dispatch_mode<24>(sc, a, grid, grid_out, s);
+  return path_dispatch_mode<32>(sc, a, grid, grid_out, s);
 }
 
-template <int STACK, int MODE, int WIDTH>
+template <int STACK, int MODE>
 hipError_t launch_bounce_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
-  if (a.classes != 2 && !use_refill<MODE, WIDTH>()) return hipErrorInvalidValue;   // 4 classes: lane-refill kernel only
   const DeviceScene f = fit_lds_nodes(sc, MODE, STACK < 0 ? -STACK : STACK, grid);
-  const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, grid, use_refill<MODE, WIDTH>());
-  if (use_refill<MODE, WIDTH>()) bounce_refill_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
-  else bounce_kernel<STACK, MODE, WIDTH><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
+  const size_t lds = bounce_lds_bytes(f, MODE, STACK < 0 ? -STACK : STACK, grid);
+  bounce_kernel<STACK, MODE><<<dim3(grid), dim3(kBlock), lds, s>>>(f, a);
   return hipGetLastError();
 }
 
-template <int STACK, int WIDTH>
+template <int STACK>
 hipError_t dispatch_mode(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
                          hipStream_t s) {
   switch (choose_mode(sc)) {
     case kAllLds:
-      return a ? launch_bounce_t<STACK, kAllLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kAllLds, WIDTH>(sc, grid, grid_out);
+      return a ? launch_bounce_t<STACK, kAllLds>(sc, *a, grid, s) : grid_for<STACK, kAllLds>(sc, grid, grid_out);
     case kTopLds:
-      return a ? launch_bounce_t<STACK, kTopLds, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kTopLds, WIDTH>(sc, grid, grid_out);
+      return a ? launch_bounce_t<STACK, kTopLds>(sc, *a, grid, s) : grid_for<STACK, kTopLds>(sc, grid, grid_out);
     default:
-      return a ? launch_bounce_t<STACK, kGlobal, WIDTH>(sc, *a, grid, s) : grid_for<STACK, kGlobal, WIDTH>(sc, grid, grid_out);
+      return a ? launch_bounce_t<STACK, kGlobal>(sc, *a, grid, s) : grid_for<STACK, kGlobal>(sc, grid, grid_out);
   }
-}
-
-template <int STACK>
-hipError_t dispatch_width(const DeviceScene& sc, const BounceArgs* a, uint32_t grid, uint32_t* grid_out,
-                          hipStream_t s) {
-  if (sc.width == 8) return dispatch_mode<STACK, 8>(sc, a, grid, grid_out, s);
-  return sc.width == 4 ? dispatch_mode<STACK, 4>(sc, a, grid, grid_out, s)
-                       : dispatch_mode<STACK, 2>(sc, a, grid, grid_out, s);
 }
 
 // stack_entries = LDS stack capacity (8/16/24/32); when the BVH's bound is
 // larger, the spill variants (8, 16 or 32 LDS entries + global) are used
 hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_entries, uint32_t grid,
                     uint32_t* grid_out, hipStream_t s) {
+  if (sc.width != 4) return hipErrorInvalidValue;
   if (sc.max_stack > stack_entries) {
-    if (stack_entries <= 8) return dispatch_width<-8>(sc, a, grid, grid_out, s);
-    if (stack_entries <= 16) return dispatch_width<-16>(sc, a, grid, grid_out, s);
-    return dispatch_width<-32>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 8) return dispatch_mode<-8>(sc, a, grid, grid_out, s);
+    if (stack_entries <= 16) return dispatch_mode<-16>(sc, a, grid, grid_out, s);
+    return dispatch_mode<-32>(sc, a, grid, grid_out, s);
   }
-  if (stack_entries <= 8) return dispatch_width<8>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 12) return dispatch_width<12>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 16) return dispatch_width<16>(sc, a, grid, grid_out, s);
-  if (stack_entries <= 24) return dispatch_width<24>(sc, a, grid, grid_out, s);
-  return dispatch_width<32>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 8) return dispatch_mode<8>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 12) return dispatch_mode<12>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 16) return dispatch_mode<16>(sc, a, grid, grid_out, s);
+  if (stack_entries <= 24) return dispatch_mode<24>(sc, a, grid, grid_out, s);
+  return dispatch_mode<32>(sc, a, grid, grid_out, s);
 }
 
-// wave-local streaming wavefront: whole-scene-in-LDS scenes, BVH2/BVH4, the
-// stack in LDS
-template <int STACK, int WIDTH>
+// wave-local streaming wavefront: whole-scene-in-LDS scenes, the stack in LDS
+template <int STACK>
 hipError_t launch_stream_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
-  stream_kernel<STACK, kAllLds, WIDTH><<<dim3(grid), dim3(kBlock), bounce_lds_bytes(sc, kAllLds, STACK, 0, false), s>>>(sc, a);
+  stream_kernel<STACK, kAllLds><<<dim3(grid), dim3(kBlock), bounce_lds_bytes(sc, kAllLds, STACK, 0), s>>>(sc, a);
   return hipGetLastError();
 }
-template <int STACK>
-hipError_t stream_width(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
-  return sc.width == 4 ? launch_stream_t<STACK, 4>(sc, a, grid, s) : launch_stream_t<STACK, 2>(sc, a, grid, s);
-}
 bool stream_ok(const DeviceScene& sc, uint32_t stack_entries) {
-  return (sc.width == 2 || sc.width == 4) && choose_mode(sc) == kAllLds && sc.max_stack <= stack_entries &&
-         stack_entries <= 32;
+  return sc.width == 4 && choose_mode(sc) == kAllLds && sc.max_stack <= stack_entries && stack_entries <= 32;
 }
 
 }  // namespace
@@ -2620,23 +1954,16 @@ hipError_t launch_raygen(uint32_t W, uint32_t H, const float* noise, RefRay* ray
 hipError_t launch_intersect(const DeviceScene& sc, const void* rays, uint32_t stride, uint32_t count,
                             RefIntersection* out, uint32_t* spill, hipStream_t s) {
   if (count == 0) return hipSuccess;
+  if (sc.width != 4) return hipErrorInvalidValue;
   const uint8_t* r = reinterpret_cast<const uint8_t*>(rays);
-  if (sc.width == 8) {   // BVH8: <= 32 levels (one group entry per level), two words per entry in LDS
-    if (sc.max_stack > 32) return hipErrorInvalidValue;
-    const size_t lds = (size_t)32 * 2 * kBlock * 4;
-    intersect_kernel<8, 32><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);
-    return hipGetLastError();
-  }
   if (sc.max_stack <= (uint32_t)kMaxStack) {   // whole stack in LDS
     const size_t lds = (size_t)kMaxStack * kBlock * 4;
-    if (sc.width == 4) intersect_kernel<4, kMaxStack><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);
-    else intersect_kernel<2, kMaxStack><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);
+    intersect_kernel<kMaxStack><<<dim3(blocks_for(count)), dim3(kBlock), lds, s>>>(sc, r, stride, count, out, nullptr);
   } else {                                      // 32 LDS entries + global spill, persistent grid
     if (!spill) return hipErrorInvalidValue;
     const size_t lds = (size_t)32 * kBlock * 4;
     const dim3 g(std::min<uint32_t>(blocks_for(count), kIntersectSpillGrid));
-    if (sc.width == 4) intersect_kernel<4, -32><<<g, dim3(kBlock), lds, s>>>(sc, r, stride, count, out, spill);
-    else intersect_kernel<2, -32><<<g, dim3(kBlock), lds, s>>>(sc, r, stride, count, out, spill);
+    intersect_kernel<-32><<<g, dim3(kBlock), lds, s>>>(sc, r, stride, count, out, spill);
   }
   return hipGetLastError();
 }
@@ -2805,18 +2132,18 @@ hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* gr
   return path_dispatch(sc, nullptr, stack_entries, 0, grid, nullptr);
 }
 
-bool path_preferred(const DeviceScene& sc) { return sc.width != 8 && choose_mode(sc) != kAllLds; }
+bool path_preferred(const DeviceScene& sc) { return choose_mode(sc) != kAllLds; }
 
 bool stream_supported(const DeviceScene& sc, uint32_t stack_entries) { return stream_ok(sc, stack_entries); }
 
 hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,
                          hipStream_t s) {
   if (!stream_ok(sc, stack_entries) || a.max_path_length > kStreamMaxL) return hipErrorNotSupported;
-  if (stack_entries <= 8) return stream_width<8>(sc, a, grid, s);
-  if (stack_entries <= 12) return stream_width<12>(sc, a, grid, s);
-  if (stack_entries <= 16) return stream_width<16>(sc, a, grid, s);
-  if (stack_entries <= 24) return stream_width<24>(sc, a, grid, s);
-  return stream_width<32>(sc, a, grid, s);
+  if (stack_entries <= 8) return launch_stream_t<8>(sc, a, grid, s);
+  if (stack_entries <= 12) return launch_stream_t<12>(sc, a, grid, s);
+  if (stack_entries <= 16) return launch_stream_t<16>(sc, a, grid, s);
+  if (stack_entries <= 24) return launch_stream_t<24>(sc, a, grid, s);
+  return launch_stream_t<32>(sc, a, grid, s);
 }
 
 }  // namespace MRT_NS

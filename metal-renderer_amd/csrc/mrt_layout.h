@@ -8,9 +8,8 @@
 //   2. the MI355X-native layouts used by the fused wavefront path:
 //        * ray queue: SoA of four float4 planes (16-B lane loads, 1 KiB per
 //          wave instruction, fully coalesced);
-//        * BVH2 nodes: 64-B records (both child boxes + child refs) so one
-//          node visit is four 16-B loads from one 64-B line; BVH4 nodes:
-//          128-B component-major records (four child boxes + refs);
+//        * BVH4 nodes: 128-B component-major records (four child boxes +
+//          refs) so one node visit is seven 16-B loads from one 128-B line;
 //        * leaf triangles: {v0|prim, e1, e2} float4 triples in leaf order;
 //        * per-primitive shading records (positions, normals, material and
 //          light ids) in primitive order so a hit gathers 6 x 16 B with no
@@ -60,11 +59,6 @@ static_assert(sizeof(RefTriangleReference) == 20, "RefTriangleReference");
 static_assert(sizeof(RefLightTriangle) == 100, "RefLightTriangle");
 
 // ---- device scene (MI355X layout) -----------------------------------------
-// BVH2 node i = nodes[4i .. 4i+3]:
-//   [0] = (L.lo.x, L.hi.x, L.lo.y, L.hi.y)
-//   [1] = (R.lo.x, R.hi.x, R.lo.y, R.hi.y)
-//   [2] = (L.lo.z, L.hi.z, R.lo.z, R.hi.z)
-//   [3] = (bits(Lref), bits(Rref), 0, 0)
 // ref >= 0: interior node index; ref < 0: leaf, ~ref = (first << 4) | (count-1)
 //
 // BVH4 node i = nodes[8i .. 8i+7] (128 B, two 64-B lines), component-major so
@@ -73,35 +67,7 @@ static_assert(sizeof(RefLightTriangle) == 100, "RefLightTriangle");
 //   [4] = lo.z[0..3]  [5] = hi.z[0..3]  [6] = bits(ref[0..3])  [7] = 0
 // Unused child slots carry ref == kEmptyChild (and a zero box); the traversal
 // masks them by ref, never by box.
-//
-// BVH8 node i = nodes[5i .. 5i+4] (80 B): compressed 8-wide node, for scenes
-// traversed from global memory (compressed wide BVH after Ylitie, Karras &
-// Laine, HPG 2017, with our own encoding):
-//   [0] = (p.x, p.y, p.z, bits(ex | ey << 8 | ez << 16 | imask << 24))
-//         p = quantisation origin, e* = per-axis exponent + 128 (scale 2^e),
-//         imask bit s = slot s holds an interior child
-//   [1] = (bits(child_base), bits(tri_base), bits(meta[0..3]), bits(meta[4..7]))
-//         interior child in slot s = node child_base + popcount(imask & ((1 << s) - 1));
-//         meta[s] of a leaf slot = (unary triangle count (1, 3, 7) << 5) | offset:
-//         triangles tri_base + offset .. (count <= 3, offset + count <= 24); 0 otherwise
-//   [2] = qlo.x[0..7], qlo.y[0..7]   (one byte per slot)
-//   [3] = qlo.z[0..7], qhi.x[0..7]
-//   [4] = qhi.y[0..7], qhi.z[0..7]
-// Child box = p + 2^e * q (exact product, one rounding in the add), rounded
-// outward at build time and checked in float, so the slab test stays
-// conservative.  Empty slots have qlo = 255 > qhi = 0 and no imask/meta bits.
-// Slots follow the octant of the child's centroid relative to the node
-// centre: a ray in octant o (bit a set where direction a < 0) visits slot
-// (k ^ o) k-th, an approximately near-to-far order without sorting.
-//
-// Quantised BVH4 node i = qnodes[4i .. 4i+3] (64 B, one 64-B line; device
-// width code 5, made from a BVH4 by quantize_bvh4 for the path kernel):
-//   [0] = (p.x, p.y, p.z, bits(ex | ey << 8 | ez << 16))   origin, exponent + 128
-//   [1] = bits(ref[0..3])                                   as the BVH4 node's
-//   [2] = (qlo.x[0..3], qhi.x[0..3], qlo.y[0..3], qhi.y[0..3])   one byte per child
-//   [3] = (qlo.z[0..3], qhi.z[0..3], 0, 0)
-// Child plane = p + 2^e * q, rounded outward from the BVH4's padded planes
-// and checked in float as for BVH8; an empty slot has qlo = 255 > qhi = 0.
+
 constexpr int32_t kEmptyChild = 0x7FFFFFFF;
 constexpr int kLeafCountBits = 4;
 constexpr int kMaxLeafSize = 1 << kLeafCountBits;   // 16
@@ -114,7 +80,7 @@ constexpr uint32_t kIntersectSpillGrid = 1024;      // persistent grid of the st
 // 16-B aligned device memory; float pointers documented as "float4" hold
 // 4 floats per record.
 struct DeviceScene {
-  const float* nodes;        // float4 x 4 (BVH2) or x 8 (BVH4) per node (see above)
+  const float* nodes;        // float4 x 8 per BVH4 node (see above)
   const float* tris;         // float4 x 3 per leaf-ordered triangle: (v0, bits(prim)), (e1, 0), (e2, 0)
   const float* prims;        // float4 x 6 per primitive (original order):
                              //   (p0, bits(material)), (p1, bits(light index or ~0u)), (p2, 0),
@@ -129,7 +95,7 @@ struct DeviceScene {
   uint32_t num_materials;
   uint32_t num_lights;       // light triangles, excluding the sentinel (SharedData.lightTrianglesCount)
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
-  uint32_t width;            // 2 = BVH2, 4 = BVH4, 8 = compressed BVH8, 5 = quantised BVH4 (path kernel)
+  uint32_t width;            // node width: 4 (BVH4; the only layout the kernels traverse)
   uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack)
 };
 
@@ -139,6 +105,6 @@ struct DeviceScene {
 #else
 #define MRT_HD
 #endif
-MRT_HD constexpr uint32_t node_float4s(uint32_t width) { return width == 8 ? 5u : width == 5 ? 4u : 2u * width; }
+MRT_HD constexpr uint32_t node_float4s(uint32_t width) { return 2u * width; }
 
 }  // namespace mrt

@@ -98,9 +98,7 @@ struct mrt_scene {
   mrt::HostScene host;
   mrt::BvhResult bvh;
   DevBuf nodes, tris, prims, materials, lights;
-  DevBuf qnodes;                // quantised BVH4 for the path kernel (BVH4 scenes only)
   mrt::DeviceScene dev{};
-  mrt::DeviceScene qdev{};      // dev with the quantised nodes (width code 5); width 0 if none
   mrt_scene_info info{};
 };
 
@@ -125,7 +123,7 @@ struct FrameSlot {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   DevBuf queue[2][4];       // ray queues (the streaming wavefront: queue[0] holds the per-wave queues)
-  DevBuf segments;          // 2 x grid per-block survivor counts + 2 chunk words
+  DevBuf segments;          // 2 queues x 2 classes x grid per-block survivor counts + 2 chunk words
   DevBuf radiance;          // W*H float4, written once per owned pixel per frame
   DevBuf spill;             // traversal stack entries beyond the LDS capacity (deep BVHs)
   hipEvent_t acc_done = nullptr;
@@ -186,12 +184,7 @@ struct mrt_renderer {
   bool stream_allowed = false;  // streaming wavefront possible for this scene / configuration
   bool stream_mode = false; // wavefront as one launch per frame batch with per-wave queues (stream_kernel)
   bool path_mode = true;   // one path-megakernel launch per frame batch (else L bounce launches, MRT_KERNEL=wave)
-  bool use_qbvh = true;    // path kernel on the quantised BVH4 when the scene has one (MRT_QBVH=1 scenes)
-  const mrt::DeviceScene& path_scene() const {
-    return use_qbvh && scene->qdev.width == 5 ? scene->qdev : scene->dev;
-  }
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
-  uint32_t classes = 2;  // material classes of the survivor partition (MRT_CLASSES=4: lane-refill kernel only)
   Exchange x;
   DevBuf reference, display;   // comparison image (mrt_renderer_load_reference) and blit output
 };
@@ -292,23 +285,21 @@ int alloc_frame_buffers(mrt_renderer* r) {
   if (owned_slots >= ((size_t)1 << 31)) return fail(MRT_ERR_INVALID, "frame too large");
   // queue capacity: every owned slot of the batch + per-block rounding and
   // slack of the segments (kernels.h)
-  const size_t slots = owned_slots * r->batch + (size_t)r->grid * (256 + mrt::kMaxSegSlack);
+  const size_t slots = owned_slots * r->batch + (size_t)r->grid * (256 + mrt::kSegSlack);
   r->stream_mode = r->stream_allowed;
   for (FrameSlot& fs : r->slots) {
-    HIP_TRY(fs.segments.alloc(((size_t)8 * r->grid + 2) * 4));   // 2 queues x 4 classes x grid + 2 chunk words
+    HIP_TRY(fs.segments.alloc(((size_t)4 * r->grid + 2) * 4));   // 2 queues x 2 classes x grid + 2 chunk words
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
     // the path kernel keeps the path state in LDS: no ray queues; the
     // streaming wavefront needs only its per-wave queues
-    const size_t qslots = r->stream_mode ? mrt::stream_slots(r->desc.max_path_length, r->grid) : slots * (r->classes / 2);
+    const size_t qslots = r->stream_mode ? mrt::stream_slots(r->desc.max_path_length, r->grid) : slots;
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < 4; ++p)
         HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (r->stream_mode && q == 1) ? 0 : qslots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
-    // spill rows of max_stack words per lane (BVH8 group entries: two words;
-    // kernels.hip LdsCtx::spill_lane)
-    const size_t spill_entries = r->scene->dev.width == 8 ? 2 * (size_t)need : (size_t)need;
-    if (need > r->stack_entries && !fs.spill.p) HIP_TRY(fs.spill.alloc(spill_entries * r->grid * 256 * 4));
+    // spill rows of max_stack words per lane (kernels.hip LdsCtx::spill_lane)
+    if (need > r->stack_entries && !fs.spill.p) HIP_TRY(fs.spill.alloc((size_t)need * r->grid * 256 * 4));
   }
   if (r->own_image) {
     if (r->image) (void)hipFree(r->image);
@@ -334,8 +325,8 @@ inline hipError_t launch_stream(const mrt_renderer* r, const mrt::BounceArgs& a,
 }
 
 inline hipError_t launch_paths(const mrt_renderer* r, const mrt::BounceArgs& a, hipStream_t s) {
-  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_paths(r->path_scene(), a, r->stack_entries, r->grid, s);
-  return mrt::fast::launch_paths(r->path_scene(), a, r->stack_entries, r->grid, s);
+  if (r->desc.flags & MRT_FLAG_PRECISE) return mrt::precise::launch_paths(r->scene->dev, a, r->stack_entries, r->grid, s);
+  return mrt::fast::launch_paths(r->scene->dev, a, r->stack_entries, r->grid, s);
 }
 
 inline hipError_t launch_accumulate_frame(const mrt_renderer* r, const mrt::AccumArgs& a, hipStream_t s) {
@@ -612,17 +603,13 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (const char* v = std::getenv("MRT_BINS")) opt.bins = (uint32_t)std::strtoul(v, nullptr, 0);
   if (const char* v = std::getenv("MRT_EXACT_SAH")) opt.exact_sah_below = (uint32_t)std::strtoul(v, nullptr, 0);
   const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
-  // default width 4: the compressed BVH8 (bvh_width = 8) halves the node
-  // bytes but measured slower on every global-memory scene (C4 -33 %, C3
-  // -26 %: 1.85x the VALU instructions per launch)
+  // BVH4 is the one layout the kernels traverse (BVH2 measured -24 %, a
+  // compressed BVH8 -33 % and a quantised BVH4 -10 % on C4 in r2)
   opt.width = desc->bvh_width ? desc->bvh_width : 4;
-  if (const char* v = std::getenv("MRT_BVH_WIDTH"); v && !desc->bvh_width) opt.width = (uint32_t)std::strtoul(v, nullptr, 0);
-  if (opt.width != 2 && opt.width != 4 && opt.width != 8) return fail(MRT_ERR_INVALID, "bvh_width must be 2, 4 or 8");
-  if (opt.width == 8 && opt.max_leaf_size > 3) opt.max_leaf_size = 3;   // BVH8 leaf slots hold <= 3 triangles
+  if (opt.width != 4) return fail(MRT_ERR_INVALID, "bvh_width must be 4 (or 0 = default)");
   if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH && builder != MRT_BVH_DEVICE_PLOC)
     return fail(MRT_ERR_INVALID, "unknown bvh_builder");
   if (builder != MRT_BVH_HOST_SAH && desc->device < 0) return fail(MRT_ERR_INVALID, "device BVH build needs a device");
-  if (builder != MRT_BVH_HOST_SAH && opt.width != 4) return fail(MRT_ERR_INVALID, "device BVH build is BVH4 only");
   double build_ms = 0.0;
   if (builder == MRT_BVH_HOST_SAH) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -737,19 +724,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.width = s->bvh.width;
   d.max_stack = s->bvh.max_stack;
   HIP_TRY(alloc_isect_spill(s->isect_spill, d.max_stack));
-  // quantised BVH4 for the path kernel: opt-in (MRT_QBVH=1). Half the node
-  // bytes, but the byte-to-float converts and per-node exponent setup cost
-  // more VALU than the fetch saves: C4 1820 -> 1636, C3 2178 -> 2137 Mpaths/s.
-  const char* qenv = std::getenv("MRT_QBVH");
-  if (qenv && std::strtoul(qenv, nullptr, 0) != 0 && s->bvh.width == 4 && s->bvh.num_nodes > 0 && s->bvh.root >= 0) {
-    std::vector<float> q;
-    if (!mrt::quantize_bvh4(s->bvh.nodes, s->bvh.num_nodes, q, err)) return fail(MRT_ERR_STATE, err);
-    HIP_TRY(upload(s->qnodes, q.data(), q.size() * 4));
-    s->qdev = d;
-    s->qdev.nodes = s->qnodes.as<float>();
-    s->qdev.width = 5;
-  }
-  in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes + s->qnodes.bytes;
+  in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
   *out = s.release();
   return MRT_OK;
 }
@@ -772,79 +747,10 @@ int mrt_scene_export(const mrt_scene* scene, void* vertices, void* indices, void
   return MRT_OK;
 }
 
-namespace {
-// Structural check of a compressed BVH8 (mrt_layout.h): every node reachable
-// once, every child box (dequantised exactly as the kernels do) inside its
-// parent's and containing its subtree's triangles, every primitive in one
-// leaf slot with the right record, stack bound = levels.
-int check_bvh8(const mrt::BvhResult& b, const mrt::HostScene& h) {
-  const uint32_t T = (uint32_t)h.references.size();
-  std::vector<uint8_t> seen(T, 0), node_seen(b.num_nodes, 0);
-  auto fb = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
-  struct Item { uint32_t node, level; float lo[3], hi[3]; };
-  std::vector<Item> st{{0u, 0u, {-1e30f, -1e30f, -1e30f}, {1e30f, 1e30f, 1e30f}}};
-  while (!st.empty()) {
-    const Item it = st.back();
-    st.pop_back();
-    if (it.node >= b.num_nodes || node_seen[it.node]) return fail(MRT_ERR_STATE, "BVH8 node out of range or reached twice");
-    node_seen[it.node] = 1;
-    if (it.level >= b.max_stack) return fail(MRT_ERR_STATE, "BVH8 stack bound too small");
-    const float* n = &b.nodes[20 * (size_t)it.node];
-    const uint32_t ew = fb(n[3]), imask = ew >> 24, child_base = fb(n[4]), tri_base = fb(n[5]);
-    const uint32_t meta[2] = {fb(n[6]), fb(n[7])};
-    uint32_t rank = 0;
-    for (uint32_t s = 0; s < 8; ++s) {
-      const uint32_t m = (meta[s >> 2] >> (8 * (s & 3))) & 0xFFu;
-      const bool internal = (imask >> s) & 1u;
-      if (!internal && m == 0) continue;
-      if (internal && m) return fail(MRT_ERR_STATE, "BVH8 slot both interior and leaf");
-      float lo[3], hi[3];
-      for (int a = 0; a < 3; ++a) {
-        const int e = (int)((ew >> (8 * a)) & 0xFFu) - 128;
-        const uint32_t w = 8 + 2 * a + (s >> 2), wh = 14 + 2 * a + (s >> 2);
-        const uint32_t ql = (fb(n[w]) >> (8 * (s & 3))) & 0xFFu, qh = (fb(n[wh]) >> (8 * (s & 3))) & 0xFFu;
-        lo[a] = n[a] + std::ldexp((float)ql, e);
-        hi[a] = n[a] + std::ldexp((float)qh, e);
-        if (!(lo[a] <= hi[a])) return fail(MRT_ERR_STATE, "BVH8 empty child box");
-      }
-      if (internal) {
-        st.push_back({child_base + rank++, it.level + 1, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
-        continue;
-      }
-      const uint32_t off = m & 31u, unary = m >> 5;
-      const uint32_t cnt = unary == 1 ? 1 : unary == 3 ? 2 : unary == 7 ? 3 : 0;
-      if (!cnt || off + cnt > 24 || tri_base + off + cnt > T) return fail(MRT_ERR_STATE, "BVH8 bad leaf slot");
-      for (uint32_t k = tri_base + off; k < tri_base + off + cnt; ++k) {
-        const float* t = &b.tris[12 * (size_t)k];
-        const uint32_t prim = fb(t[3]);
-        if (prim >= T || seen[prim]) return fail(MRT_ERR_STATE, "BVH primitive missing or duplicated");
-        seen[prim] = 1;
-        const float* v[3] = {h.vertices[h.references[prim].tri[0]].v, h.vertices[h.references[prim].tri[1]].v,
-                             h.vertices[h.references[prim].tri[2]].v};
-        for (int c = 0; c < 3; ++c)
-          for (int a = 0; a < 3; ++a)
-            if (!(v[c][a] >= lo[a] && v[c][a] <= hi[a])) return fail(MRT_ERR_STATE, "BVH box does not contain its triangle");
-        for (int a = 0; a < 3; ++a)
-          if (t[a] != v[0][a] || t[4 + a] != v[1][a] - v[0][a] || t[8 + a] != v[2][a] - v[0][a])
-            return fail(MRT_ERR_STATE, "BVH leaf triangle record mismatch");
-      }
-    }
-    if (rank != (uint32_t)__builtin_popcount(imask)) return fail(MRT_ERR_STATE, "BVH8 interior child count");
-    (void)it.lo;
-  }
-  for (uint32_t t = 0; t < T; ++t)
-    if (!seen[t]) return fail(MRT_ERR_STATE, "BVH primitive not referenced");
-  for (uint32_t k = 0; k < b.num_nodes; ++k)
-    if (!node_seen[k]) return fail(MRT_ERR_STATE, "BVH has unreachable nodes");
-  return MRT_OK;
-}
-}  // namespace
-
 int mrt_scene_check_bvh(const mrt_scene* scene) {
   if (!scene) return fail(MRT_ERR_INVALID, "null scene");
   const mrt::BvhResult& b = scene->bvh;
   const mrt::HostScene& h = scene->host;
-  if (b.width == 8) return check_bvh8(b, h);
   const uint32_t T = (uint32_t)h.references.size();
   std::vector<uint8_t> seen(T, 0);
   auto fbits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
@@ -864,11 +770,7 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
       ++nodes_seen;
       Item ch[4];
       uint32_t nc = 0;
-      if (b.width == 2) {
-        const float* n = &b.nodes[16 * (size_t)it.ref];
-        ch[nc++] = Item{(int32_t)fbits(n[12]), {n[0], n[2], n[8]}, {n[1], n[3], n[9]}, it.depth + 1, 0};
-        ch[nc++] = Item{(int32_t)fbits(n[13]), {n[4], n[6], n[10]}, {n[5], n[7], n[11]}, it.depth + 1, 0};
-      } else {
+      {
         const float* n = &b.nodes[32 * (size_t)it.ref];
         for (int c = 0; c < 4; ++c) {
           const int32_t ref = (int32_t)fbits(n[24 + c]);
@@ -1151,15 +1053,12 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   // bounces of a frame batch in one launch: C3 +15 %, C4 +1.5 % over the
   // wavefront), scenes staged whole in LDS the wavefront of per-bounce
   // launches (C2: the path kernel is 24 % slower); MRT_KERNEL=path|wave
-  // overrides.  The compressed BVH8 is traversed by the wavefront kernels only.
+  // overrides.
   r->path_mode = mrt::fast::path_preferred(desc->scene->dev);
-  if (const char* k = std::getenv("MRT_KERNEL"))
-    r->path_mode = desc->scene->dev.width != 8 && std::strcmp(k, "path") == 0;
-  // the path kernel reads the quantised BVH4 (64-B node fetches) when the
-  // scene was created with one (MRT_QBVH=1)
+  if (const char* k = std::getenv("MRT_KERNEL")) r->path_mode = std::strcmp(k, "path") == 0;
   if (r->path_mode)
-    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::path_grid(r->path_scene(), r->stack_entries, &r->grid)
-                                             : mrt::fast::path_grid(r->path_scene(), r->stack_entries, &r->grid));
+    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::path_grid(r->scene->dev, r->stack_entries, &r->grid)
+                                             : mrt::fast::path_grid(r->scene->dev, r->stack_entries, &r->grid));
   else
     HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid)
                                              : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid));
@@ -1172,10 +1071,6 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     r->stream_allowed = want && !r->path_mode && desc->max_path_length <= mrt::kStreamMaxL &&
                         mrt::fast::stream_supported(desc->scene->dev, r->stack_entries);
   }
-  // four-way material re-sort (one class per BSDF) for the lane-refill
-  // wavefront of global-memory scenes; measured, not the default
-  if (const char* c = std::getenv("MRT_CLASSES"))
-    if (std::atoi(c) == 4 && !r->path_mode && mrt::fast::path_preferred(desc->scene->dev)) r->classes = 4;
   int rc = alloc_frame_buffers(r.get());
   if (rc) return rc;
   *out = r.release();
@@ -1247,7 +1142,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     const uint32_t batch = std::min<uint32_t>(B, n - k * B);
     FrameSlot& fs = r->slots[k % r->inflight];
     uint32_t* seg = fs.segments.as<uint32_t>();
-    uint32_t* meta = seg + 8 * (size_t)r->grid;
+    uint32_t* meta = seg + 4 * (size_t)r->grid;
     for (uint32_t b = 0; b < launches_per_batch; ++b) {
       mrt::BounceArgs a{};
       a.width = r->desc.width;
@@ -1261,11 +1156,10 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.tiles_x = r->tiles_x;
       a.num_slots = r->owned_tiles * 4096u;
       a.debug = r->debug;
-      a.classes = r->classes;
-      a.in_segments = r->classes * r->grid;   // material classes per block
-      a.in_seg_count = seg + (size_t)((b + 1) & 1) * 4 * r->grid;
+      a.in_segments = 2 * r->grid;   // two material classes per block
+      a.in_seg_count = seg + (size_t)((b + 1) & 1) * 2 * r->grid;
       a.in_chunk = meta + ((b + 1) & 1);
-      a.out_seg_count = seg + (size_t)(b & 1) * 4 * r->grid;
+      a.out_seg_count = seg + (size_t)(b & 1) * 2 * r->grid;
       a.out_chunk = meta + (b & 1);
       a.out_total = cnt + (size_t)k * L + b;
       a.grab = r->grabs.as<uint32_t>() + ((size_t)k * L + b) * grab_words;

@@ -53,12 +53,11 @@ def test_c2_full_size_matches_oracle(gpu, mrt_mod, c2_oracle, build):
         assert abs(st["active_ray_bounces"] - A) <= A // 1000
 
 
-@pytest.fixture(scope="module", params=[4, 8], ids=["bvh4", "bvh8"])
-def big_scene(gpu, mrt_mod, oracle_mod, request):
+@pytest.fixture(scope="module")
+def big_scene(gpu, mrt_mod, oracle_mod):
     """C4/C5's scene: cornellbox + the seeded 1M-triangle displaced sphere
-    (host SAH BVH4, the default, and the compressed BVH8), and the oracle
-    over the same flattened buffers."""
-    sc = mrt_mod.Scene("cornellbox", procedural_triangles=PROC, bvh_width=request.param)
+    (host SAH BVH4), and the oracle over the same flattened buffers."""
+    sc = mrt_mod.Scene("cornellbox", procedural_triangles=PROC)
     e = sc.export()
     osc = oracle_mod.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
     assert sc.info["triangles"] == PROC + 36
@@ -147,50 +146,33 @@ def test_frames_in_flight_bitwise(gpu, mrt_mod, monkeypatch, inflight):
 
 
 @pytest.mark.parametrize("build", ["precise", "fast"])
-def test_quantised_bvh4_path_kernel_bitwise(gpu, mrt_mod, monkeypatch, build):
-    """MRT_QBVH=1 (opt-in): the path kernel on the 64-B quantised BVH4 nodes
-    renders bitwise like the float BVH4 (outward-rounded boxes only add
-    visits; hits are the triangles' own)."""
-    imgs = []
-    for q in ("0", "1"):
-        monkeypatch.setenv("MRT_QBVH", q)
-        sc = mrt_mod.Scene("cornellbox", procedural_triangles=1 << 16)
-        r = mrt_mod.Renderer(sc, 96, 64, 4, precise=(build == "precise"))
-        assert r.stats()["kernel"] == 1
-        r.draw(2)
-        imgs.append(r.read_image())
-        r.close()
-        sc.close()
-    assert np.isfinite(imgs[0]).all()
-    assert np.array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
-
-
-@pytest.mark.parametrize("build", ["precise", "fast"])
-def test_four_class_resort_bitwise(gpu, mrt_mod, monkeypatch, tmp_path, build):
-    """MRT_CLASSES=4 (measured, opt-in): the lane-refill wavefront partitions
-    survivors by the BSDF they leave (diffuse / mirror / plastic / dielectric,
-    renderer/KernelHelpers.h:63-111,126-173) instead of diffuse vs the rest.
-    On the scene with all four BSDFs (C3g: the water as a dielectric) the
-    image and the active-ray counts equal the two-class wavefront and the
-    path kernel bitwise (rays carry their pixel; order never changes a path)."""
+def test_path_kernel_equals_wavefront(gpu, mrt_mod, monkeypatch, tmp_path, build):
+    """The path megakernel (the product's kernel for scenes traversed from
+    global memory) against the wavefront of per-bounce launches
+    (MRT_KERNEL=wave: the reference's per-bounce structure, survivors
+    re-sorted by material between bounces) on the scene with all four BSDFs
+    (C3g: the water as a dielectric, renderer/KernelHelpers.h:63-111,126-173):
+    the same image and active-ray counts bitwise (rays carry their pixel;
+    order never changes a path).  Precise: both are the oracle's arithmetic."""
     src = open(mrt_mod.scene_path("CornellBox-Water-plastic")[:-4] + ".mtl").read()
     mtl = tmp_path / "glass-water.mtl"
     mtl.write_text(src.replace("Ks 0.0 0.0 -1.33333", "Ks 0.0 0.0 1.33333"))
     sc = mrt_mod.Scene("CornellBox-Water-plastic", str(mtl))
     out = {}
-    for kernel, classes in (("path", "2"), ("wave", "2"), ("wave", "4")):
+    for kernel in ("path", "wave"):
         monkeypatch.setenv("MRT_KERNEL", kernel)
-        monkeypatch.setenv("MRT_CLASSES", classes)
         monkeypatch.setenv("MRT_BATCH", "2")
         r = mrt_mod.Renderer(sc, 160, 120, 8, precise=(build == "precise"))
+        assert r.stats()["kernel"] == (1 if kernel == "path" else 0)
         r.draw(3)
-        out[(kernel, classes)] = (r.read_image(), r.stats()["active_ray_bounces"])
+        out[kernel] = (r.read_image(), r.stats()["active_ray_bounces"])
         r.close()
-    # precise: every kernel bitwise like the oracle's arithmetic; fast: the
-    # two partitions run the same per-ray code (the path kernel may contract
-    # differently, so it is held to the fast-build parity only elsewhere)
-    ref = out[("path", "2")] if build == "precise" else out[("wave", "2")]
+    ref = out["path"]
     assert np.isfinite(ref[0]).all() and ref[0][..., :3].max() > 0
-    for key in (("wave", "2"), ("wave", "4")):
-        assert out[key][1] == ref[1], key
-        assert out[key][0].tobytes() == ref[0].tobytes(), key
+    if build == "precise":
+        assert out["wave"][1] == ref[1]
+        assert out["wave"][0].tobytes() == ref[0].tobytes()
+    else:   # the two kernels may contract the same expressions differently
+        assert abs(out["wave"][1] - ref[1]) <= ref[1] // 1000
+        rel = np.abs(out["wave"][0] - ref[0]).max(-1) / (np.abs(ref[0]).max(-1) + 1e-3)
+        assert np.mean(rel <= 1e-2) >= 0.99

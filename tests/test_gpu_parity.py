@@ -14,10 +14,10 @@ from helpers import SEED, dev_ptr, from_dev, pixel_metrics, to_dev
 pytestmark = pytest.mark.gpu
 
 
-def _scene(mrt_mod, name, width=4, cache={}):
-    if (name, width) not in cache:
-        cache[(name, width)] = mrt_mod.Scene(name, bvh_width=width)
-    return cache[(name, width)]
+def _scene(mrt_mod, name, cache={}):
+    if name not in cache:
+        cache[name] = mrt_mod.Scene(name)
+    return cache[name]
 
 
 def _oscene(oracle_mod, mrt_mod, name, cache={}):
@@ -56,11 +56,10 @@ def _random_rays(oracle_mod, n, rng):
 
 @pytest.mark.parametrize("scene", ["cornellbox", "white-box", "CornellBox-Water-plastic"])
 @pytest.mark.parametrize("precise", [True, False])
-@pytest.mark.parametrize("width", [2, 4, 8])
-def test_intersect_matches_bruteforce(gpu, mrt_mod, oracle_mod, scene, precise, width):
-    """BVH2, BVH4 and compressed BVH8 traversal == brute-force MPS nearest-hit
-    semantics (t, primitive, u, v)."""
-    sc, osc = _scene(mrt_mod, scene, width), _oscene(oracle_mod, mrt_mod, scene)
+def test_intersect_matches_bruteforce(gpu, mrt_mod, oracle_mod, scene, precise):
+    """BVH4 traversal == brute-force MPS nearest-hit semantics (t, primitive,
+    u, v)."""
+    sc, osc = _scene(mrt_mod, scene), _oscene(oracle_mod, mrt_mod, scene)
     rng = np.random.default_rng(7)
     # NumPy 2 repacks padded structured dtypes in concatenate: restore the 80-B layout
     rays = np.concatenate([_random_rays(oracle_mod, 6000, rng),
@@ -143,9 +142,8 @@ def _render_gpu(mrt_mod, sc, W, H, L, frames, precise, shard=(0, 1), seed=SEED):
     ("CornellBox-Water-plastic", 48, 36, 8, 2),
     ("CornellBox-Water-mirror", 40, 30, 3, 2),
 ])
-@pytest.mark.parametrize("width", [2, 4, 8])
-def test_render_parity_precise(gpu, mrt_mod, oracle_mod, scene, W, H, L, frames, width):
-    sc, osc = _scene(mrt_mod, scene, width), _oscene(oracle_mod, mrt_mod, scene)
+def test_render_parity_precise(gpu, mrt_mod, oracle_mod, scene, W, H, L, frames):
+    sc, osc = _scene(mrt_mod, scene), _oscene(oracle_mod, mrt_mod, scene)
     ref, A_ref = osc.render(W, H, L, SEED, frames, threads=8)
     img, st = _render_gpu(mrt_mod, sc, W, H, L, frames, precise=True)
     rel, rmse, same = pixel_metrics(img, ref)

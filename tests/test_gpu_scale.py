@@ -17,12 +17,11 @@ from helpers import SEED, compare_to_golden, dev_ptr, from_dev, pixel_metrics, t
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[2, 4, 8], ids=["bvh2", "bvh4", "bvh8"])
-def proc_scenes(request, gpu, mrt_mod, oracle_mod):
+@pytest.fixture(scope="module")
+def proc_scenes(gpu, mrt_mod, oracle_mod):
     """cornellbox + an 8192-triangle procedural sphere, product and oracle
     built from the same flattened buffers."""
-    sc = mrt_mod.Scene("cornellbox", procedural_triangles=8192, procedural_seed=11, lds_nodes=64,
-                       bvh_width=request.param)
+    sc = mrt_mod.Scene("cornellbox", procedural_triangles=8192, procedural_seed=11, lds_nodes=64)
     e = sc.export()
     osc = oracle_mod.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
     assert sc.info["bvh_nodes"] > sc.info["bvh_lds_nodes"] > 0   # top levels in LDS, the rest global
