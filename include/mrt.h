@@ -59,6 +59,15 @@ typedef enum mrt_status {
 #define MRT_FLAG_PRECISE 1u   /* parity kernels: IEEE div/sqrt, no FMA contraction, CR sin/cos */
 #define MRT_FLAG_PROFILE 2u   /* time the bounce launches of every 8th frame with HIP events (mrt_stats.kernel_ms);
                                  timing events serialise a stream's launches, so only a sample is timed */
+/* The reference's compile-time switches as runtime flags (renderer/Raytracing.h:11-33,
+ * renderer/Shaders.metal:7); the defaults (flag clear) are the reference's defaults. */
+#define MRT_FLAG_STATIC_NOISE 4u      /* ANIMATE_NOISE 0 (Raytracing.h:20): every frame reads the initial noise
+                                         table (Renderer.mm:109-129; :485-497 skipped).  Renderer flag. */
+#define MRT_FLAG_NO_ACCUMULATE 8u     /* ACCUMULATE_IMAGE false (Raytracing.h:14, Shaders.metal:241): the image
+                                         holds the last frame's radiance alone.  Renderer and mrt_accumulate. */
+#define MRT_FLAG_DEBUG_MATERIAL 16u   /* DEBUG_MATERIAL 1 (Shaders.metal:7,142-147): at each hit the path radiance
+                                         is set to fresnel(n, -wI, 1.0, 1.5) before emission and NEE add to it.
+                                         Renderer and mrt_shade. */
 
 typedef struct mrt_scene mrt_scene;
 typedef struct mrt_renderer mrt_renderer;

@@ -67,6 +67,7 @@ struct BounceArgs {
   uint32_t max_path_length;    // MAX_PATH_LENGTH
   uint32_t shard_rank, shard_count, tiles_x;
   uint32_t num_slots;          // per frame: owned tiles * 4096 pixel slots (bounce 0 input = num_slots * batch)
+  uint32_t flags;              // kShadeDebugMaterial: DEBUG_MATERIAL (renderer/Shaders.metal:7,142-147)
   uint32_t debug;              // ablation bits for profiling (0 in production, env MRT_DEBUG):
                                //   1 = skip shadow traversal, 2 = skip shading, 4 = no queue writes,
                                //   8 = static interleaved work assignment (no grab counters),
@@ -104,7 +105,10 @@ struct AccumArgs {
   uint32_t num_slots;          // owned tiles * 4096
   const float4* radiance;      // [batch][num_slots]
   float4* image;
+  uint32_t accumulate;         // ACCUMULATE_IMAGE (renderer/Raytracing.h:14); 0: the last frame alone
 };
+
+constexpr uint32_t kShadeDebugMaterial = 1u;   // BounceArgs::flags / launch_shade flags
 
 #define MRT_DECLARE_LAUNCHERS(NS)                                                                         \
   namespace NS {                                                                                          \
@@ -114,11 +118,11 @@ struct AccumArgs {
                               RefIntersection* out, uint32_t* spill, hipStream_t s);                      \
   hipError_t launch_shade(const DeviceScene& sc, uint32_t W, uint32_t H, uint32_t frame_index,            \
                           uint32_t max_path_length, const float* noise, const RefIntersection* isect,     \
-                          RefRay* rays, RefShadowRay* srays, hipStream_t s);                              \
+                          RefRay* rays, RefShadowRay* srays, uint32_t flags, hipStream_t s);              \
   hipError_t launch_resolve(uint32_t count, const RefIntersection* isect, RefRay* rays,                   \
                             const RefShadowRay* srays, hipStream_t s);                                    \
   hipError_t launch_accumulate(uint32_t W, uint32_t H, uint32_t frame_index, const RefRay* rays,          \
-                               float* image, hipStream_t s);                                              \
+                               float* image, bool accumulate, hipStream_t s);                             \
   /* persistent grid size of the fused bounce kernel for this scene */                                    \
   hipError_t bounce_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t blocks_per_cu,          \
                          uint32_t* grid);                                                                \

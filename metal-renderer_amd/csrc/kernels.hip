@@ -800,7 +800,8 @@ __device__ __forceinline__ uint32_t shade_noise_cell(uint32_t x, uint32_t y, uin
 // the next bounce and updates the throughput.
 template <int MODE>
 __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& cx, const Hit& h, PathState& s,
-                                          const float4& ns, uint32_t bounce, uint32_t L, bool next, ShadowRay& sh) {
+                                          const float4& ns, uint32_t bounce, uint32_t L, bool next, ShadowRay& sh,
+                                          bool debug_material) {
   // Loads are staged behind scheduling barriers: hoisting all 13 float4
   // record loads together would pin ~50 VGPRs and halve occupancy.
   // interpolate(float2) — KernelHelpers.h:23-47
@@ -823,6 +824,10 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
   MRT_SHADE_BARRIER();
   const Mat m = load_material<MODE>(sc, cx, mat_index);
   const V3 wI = s.d;
+  if (debug_material) {   // DEBUG_MATERIAL (Shaders.metal:7,142-147): radiance := Fresnel, emission and NEE add to it
+    const float f = fresnel(hn, neg(wI), 1.0f, 1.5f);
+    s.R = mk(f, f, f);
+  }
   sh.valid = false;
   // light sampling — Shaders.metal:150-176
   if (bounce + 1 < L) {
@@ -1098,7 +1103,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
       s.o = add(s.o, mul(s.d, h.t * 0.999f));
       s.d = mk(-s.d.x, -s.d.y, -s.d.z);
     } else {
-      shade_hit<MODE>(sc, cx, h, s, ns, bounce, a.max_path_length, !last, sh);
+      shade_hit<MODE>(sc, cx, h, s, ns, bounce, a.max_path_length, !last, sh, (a.flags & kShadeDebugMaterial) != 0);
     }
   }
   STAMP_AT(st, 2);
@@ -1570,7 +1575,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
         const uint32_t back = (bounce % 3u) == 0 ? 0u : ((bounce % 3u) == 1 ? 2u : 1u);
         const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, bounce, a.frame_index + fj)];
-        shade_hit<MODE>(sc, cx, h, s, ns, bounce, L, !last, sh);
+        shade_hit<MODE>(sc, cx, h, s, ns, bounce, L, !last, sh, (a.flags & kShadeDebugMaterial) != 0);
       }
       if (!hit_ok || last) {   // the path ends: accumulateImage input (Shaders.metal:233-249)
         a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
@@ -1635,8 +1640,13 @@ __global__ __launch_bounds__(kBlock) void accumulate_frame_kernel(AccumArgs a) {
     // the running mean stays in registers across the batch's frames (one
     // image read and one write per pixel); radiance rows are read once,
     // eight frames' loads in flight at a time
-    float4 cur = a.frame_index > 0 ? a.image[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const float4* rad = a.radiance + idx;
+    if (!a.accumulate) {   // ACCUMULATE_IMAGE false (Shaders.metal:241): the batch's last frame alone
+      const float4 c = rad[(size_t)(a.batch - 1) * a.num_slots];
+      a.image[pix] = make_float4(c.x, c.y, c.z, 1.0f);
+      continue;
+    }
+    float4 cur = a.frame_index > 0 ? a.image[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     uint32_t j = 0;
     for (; j + 8 <= a.batch; j += 8) {
       float4 c[8];
@@ -1696,7 +1706,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DeviceScene sc, const
 __global__ __launch_bounds__(kBlock) void shade_kernel(DeviceScene sc, uint32_t W, uint32_t H, uint32_t f,
                                                        uint32_t L, const float4* noise,
                                                        const RefIntersection* isect, RefRay* rays,
-                                                       RefShadowRay* srays) {
+                                                       RefShadowRay* srays, uint32_t flags) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= W * H) return;
   const uint32_t x = i % W, y = i / W;
@@ -1718,7 +1728,8 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DeviceScene sc, uint32_t 
   h.t = is.distance; h.prim = is.triangleIndex; h.u = is.coordinates[0]; h.v = is.coordinates[1]; h.found = true;
   ShadowRay sh;
   const LdsCtx cx = stage_lds<kGlobal>(sc, 0);
-  shade_hit<kGlobal>(sc, cx, h, s, noise[shade_noise_cell(x, y, bounce, f)], bounce, L, true, sh);
+  shade_hit<kGlobal>(sc, cx, h, s, noise[shade_noise_cell(x, y, bounce, f)], bounce, L, true, sh,
+                     (flags & kShadeDebugMaterial) != 0);
   if (bounce + 1 < L) {
     sr.origin[0] = sh.o.x; sr.origin[1] = sh.o.y; sr.origin[2] = sh.o.z;
     sr.direction[0] = sh.d.x; sr.direction[1] = sh.d.y; sr.direction[2] = sh.d.z;
@@ -1745,10 +1756,10 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(uint32_t count, const R
 }
 
 __global__ __launch_bounds__(kBlock) void accumulate_kernel(uint32_t W, uint32_t H, uint32_t f, const RefRay* rays,
-                                                            float4* image) {
+                                                            float4* image, bool accumulate) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= W * H) return;
-  accumulate_pixel(image, i, mk(rays[i].radiance[0], rays[i].radiance[1], rays[i].radiance[2]), f);
+  accumulate_pixel(image, i, mk(rays[i].radiance[0], rays[i].radiance[1], rays[i].radiance[2]), accumulate ? f : 0u);
 }
 
 inline uint32_t blocks_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
@@ -1970,9 +1981,9 @@ hipError_t launch_intersect(const DeviceScene& sc, const void* rays, uint32_t st
 
 hipError_t launch_shade(const DeviceScene& sc, uint32_t W, uint32_t H, uint32_t frame_index, uint32_t max_path_length,
                         const float* noise, const RefIntersection* isect, RefRay* rays, RefShadowRay* srays,
-                        hipStream_t s) {
+                        uint32_t flags, hipStream_t s) {
   shade_kernel<<<dim3(blocks_for(W * H)), dim3(kBlock), 0, s>>>(sc, W, H, frame_index,
-                     max_path_length, reinterpret_cast<const float4*>(noise), isect, rays, srays);
+                     max_path_length, reinterpret_cast<const float4*>(noise), isect, rays, srays, flags);
   return hipGetLastError();
 }
 
@@ -1984,9 +1995,9 @@ hipError_t launch_resolve(uint32_t count, const RefIntersection* isect, RefRay* 
 }
 
 hipError_t launch_accumulate(uint32_t W, uint32_t H, uint32_t frame_index, const RefRay* rays, float* image,
-                             hipStream_t s) {
+                             bool accumulate, hipStream_t s) {
   accumulate_kernel<<<dim3(blocks_for(W * H)), dim3(kBlock), 0, s>>>(W, H, frame_index, rays,
-                     reinterpret_cast<float4*>(image));
+                     reinterpret_cast<float4*>(image), accumulate);
   return hipGetLastError();
 }
 

@@ -244,8 +244,9 @@ int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
-      for (int64_t k = t; k < count; k += nt)
-        mrt::make_noise_table(r->desc.seed, lo + k < 0 ? -1 : lo + k, host.data() + (size_t)k * mrt::kNoiseFloats);
+      for (int64_t k = t; k < count; k += nt)   // MRT_FLAG_STATIC_NOISE (ANIMATE_NOISE 0): the initial table for every frame
+        mrt::make_noise_table(r->desc.seed, lo + k < 0 || (r->desc.flags & MRT_FLAG_STATIC_NOISE) ? -1 : lo + k,
+                              host.data() + (size_t)k * mrt::kNoiseFloats);
     });
   for (auto& x : th) x.join();
   { int rc = finalize_pending(r); if (rc) return rc; }
@@ -972,7 +973,8 @@ int mrt_shade(const mrt_scene* scene, uint32_t W, uint32_t H, uint32_t frame_ind
   if (!scene || !noise || !isect || !rays || !srays || W == 0 || H == 0 || L == 0)
     return fail(MRT_ERR_INVALID, "mrt_shade: bad argument");
   STAGE_CALL(launch_shade(scene->dev, W, H, frame_index, L, noise, (const mrt::RefIntersection*)isect,
-                          (mrt::RefRay*)rays, (mrt::RefShadowRay*)srays, (hipStream_t)stream));
+                          (mrt::RefRay*)rays, (mrt::RefShadowRay*)srays,
+                          (flags & MRT_FLAG_DEBUG_MATERIAL) ? mrt::kShadeDebugMaterial : 0u, (hipStream_t)stream));
   return MRT_OK;
 }
 
@@ -987,7 +989,8 @@ int mrt_resolve_shadow(const mrt_scene* scene, uint32_t count, const void* isect
 int mrt_accumulate(const mrt_scene* scene, uint32_t W, uint32_t H, uint32_t frame_index, const void* rays,
                    float* image, uint32_t flags, void* stream) {
   if (!scene || !rays || !image || W == 0 || H == 0) return fail(MRT_ERR_INVALID, "mrt_accumulate: bad argument");
-  STAGE_CALL(launch_accumulate(W, H, frame_index, (const mrt::RefRay*)rays, image, (hipStream_t)stream));
+  STAGE_CALL(launch_accumulate(W, H, frame_index, (const mrt::RefRay*)rays, image, !(flags & MRT_FLAG_NO_ACCUMULATE),
+                               (hipStream_t)stream));
   return MRT_OK;
 }
 
@@ -1004,6 +1007,9 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     return fail(MRT_ERR_INVALID, "max_path_length must be in [1, 64]");
   const uint32_t S = std::max<uint32_t>(1, desc->shard_count);
   if (desc->shard_rank >= S) return fail(MRT_ERR_INVALID, "shard_rank >= shard_count");
+  constexpr uint32_t kKnownFlags = MRT_FLAG_PRECISE | MRT_FLAG_PROFILE | MRT_FLAG_STATIC_NOISE |
+                                   MRT_FLAG_NO_ACCUMULATE | MRT_FLAG_DEBUG_MATERIAL;
+  if (desc->flags & ~kKnownFlags) return fail(MRT_ERR_INVALID, "unknown renderer flags");
   std::unique_ptr<mrt_renderer> r(new mrt_renderer());
   r->scene = desc->scene;
   r->desc = *desc;
@@ -1156,6 +1162,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.tiles_x = r->tiles_x;
       a.num_slots = r->owned_tiles * 4096u;
       a.debug = r->debug;
+      a.flags = (r->desc.flags & MRT_FLAG_DEBUG_MATERIAL) ? mrt::kShadeDebugMaterial : 0u;
       a.in_segments = 2 * r->grid;   // two material classes per block
       a.in_seg_count = seg + (size_t)((b + 1) & 1) * 2 * r->grid;
       a.in_chunk = meta + ((b + 1) & 1);
@@ -1193,6 +1200,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     acc.num_slots = r->owned_tiles * 4096u;
     acc.radiance = fs.radiance.as<float4>();
     acc.image = reinterpret_cast<float4*>(r->image);
+    acc.accumulate = (r->desc.flags & MRT_FLAG_NO_ACCUMULATE) ? 0u : 1u;
     HIP_TRY(launch_accumulate_frame(r, acc, fs.stream));
     HIP_TRY(hipEventRecord(fs.acc_done, fs.stream));
     prev = &fs;

@@ -37,6 +37,10 @@ SCENES_DIR = os.path.join(HERE, "scenes")   # renderer/Media scene data, rendere
 
 FLAG_PRECISE = 1
 FLAG_PROFILE = 2
+# the reference's compile-time switches (renderer/Raytracing.h:14,20; Shaders.metal:7)
+FLAG_STATIC_NOISE = 4       # ANIMATE_NOISE 0
+FLAG_NO_ACCUMULATE = 8      # ACCUMULATE_IMAGE false
+FLAG_DEBUG_MATERIAL = 16    # DEBUG_MATERIAL 1
 COMM_ID_BYTES = 128
 EXCHANGE_GATHER, EXCHANGE_REDUCE, EXCHANGE_OVERLAP = 1, 2, 0x100
 DEFAULT_SEED = 0x6D6574616C2D7274  # "metal-rt"
@@ -327,10 +331,16 @@ class Renderer:
 
     def __init__(self, scene: Scene, width: int, height: int, max_path_length: int = 8, *,
                  seed: int = DEFAULT_SEED, shard_rank: int = 0, shard_count: int = 1, precise: bool = False,
-                 profile: bool = False, stream: int | None = None, image_ptr: int | None = None):
+                 profile: bool = False, stream: int | None = None, image_ptr: int | None = None,
+                 animate_noise: bool = True, accumulate_image: bool = True, debug_material: bool = False):
+        """animate_noise / accumulate_image / debug_material: the reference's
+        ANIMATE_NOISE, ACCUMULATE_IMAGE and DEBUG_MATERIAL switches (defaults =
+        the reference's defaults)."""
         self._h = None
         self.scene = scene  # keep alive
-        flags = (FLAG_PRECISE if precise else 0) | (FLAG_PROFILE if profile else 0)
+        flags = ((FLAG_PRECISE if precise else 0) | (FLAG_PROFILE if profile else 0) |
+                 (0 if animate_noise else FLAG_STATIC_NOISE) | (0 if accumulate_image else FLAG_NO_ACCUMULATE) |
+                 (FLAG_DEBUG_MATERIAL if debug_material else 0))
         d = RendererDesc(scene.handle, width, height, max_path_length, seed, shard_rank, shard_count, flags,
                          stream, image_ptr)
         h = ctypes.c_void_p()
@@ -464,9 +474,10 @@ def intersect(scene: Scene, rays_ptr: int, stride: int, count: int, isect_ptr: i
 
 
 def shade(scene: Scene, width, height, frame_index, max_path_length, noise_ptr, isect_ptr, rays_ptr, srays_ptr,
-          precise=True, stream=None, sync=True):
+          precise=True, stream=None, sync=True, debug_material=False):
+    flags = _flags(precise) | (FLAG_DEBUG_MATERIAL if debug_material else 0)
     _check(lib().mrt_shade(scene.handle, width, height, frame_index, max_path_length, noise_ptr, isect_ptr, rays_ptr,
-                           srays_ptr, _flags(precise), stream), "mrt_shade")
+                           srays_ptr, flags, stream), "mrt_shade")
     if sync:
         synchronize(stream)
 
@@ -478,8 +489,10 @@ def resolve_shadow(scene: Scene, count, isect_ptr, rays_ptr, srays_ptr, precise=
         synchronize(stream)
 
 
-def accumulate(scene: Scene, width, height, frame_index, rays_ptr, image_ptr, precise=True, stream=None, sync=True):
-    _check(lib().mrt_accumulate(scene.handle, width, height, frame_index, rays_ptr, image_ptr, _flags(precise),
+def accumulate(scene: Scene, width, height, frame_index, rays_ptr, image_ptr, precise=True, stream=None, sync=True,
+               accumulate_image=True):
+    flags = _flags(precise) | (0 if accumulate_image else FLAG_NO_ACCUMULATE)
+    _check(lib().mrt_accumulate(scene.handle, width, height, frame_index, rays_ptr, image_ptr, flags,
                                 stream), "mrt_accumulate")
     if sync:
         synchronize(stream)

@@ -33,6 +33,7 @@
 // and rounded to float (correctly rounded in practice).  MSL float literals
 // are single precision (all constants below carry an f suffix).
 // ============================================================================
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -128,6 +129,21 @@ struct Scene {
   // intersect_packet).  The same float values tri_hit derives per test.
   mutable std::once_flag soa_once;
   mutable std::vector<float> soa;   // [9][T]
+  // A binary SAH BVH over the same triangles for the CPU baseline (SURVEY.md
+  // 8(d): "same BVH" as the GPU path rather than brute force), built on first
+  // use (see build_cpu_bvh / intersect_bvh).
+  mutable std::once_flag bvh_once;
+  mutable std::vector<struct CpuBvhNode> bvh;
+  mutable std::vector<uint32_t> bvh_prims;
+};
+
+// BVH node of the CPU baseline: a padded box and either two children
+// (count == 0: left child = node + 1, right = `right`) or a leaf of `count`
+// triangles bvh_prims[first .. first + count).
+struct CpuBvhNode {
+  float lo[3], hi[3];
+  uint32_t right_or_first;
+  uint32_t count;
 };
 
 struct MtlColor { float r = 0, g = 0, b = 0; bool set = false; };
@@ -357,6 +373,161 @@ static Intersection intersect_one(const Scene& sc, const float* o3, float tmin, 
     if (!tri_hit(o, d, f3(sc.vertices[tri[0]].v), f3(sc.vertices[tri[1]].v), f3(sc.vertices[tri[2]].v),
                  tmin, tmax, t, u, v)) continue;
     if (!found || t < bt) { found = true; bt = t; bu = u; bv = v; bk = (uint32_t)k; }
+  }
+  if (found) { r.distance = bt; r.triangleIndex = bk; r.coordinates[0] = bu; r.coordinates[1] = bv; }
+  return r;
+}
+
+// ---- CPU baseline traversal: binned-SAH BVH2 (own build, scalar) ----------
+// Conservative boxes (padded outward as the GPU builder pads, bvh.cpp) and
+// the same per-triangle test (tri_hit) with the brute force's tie rule
+// (nearest t, then lowest primitive index), so intersect_bvh returns exactly
+// intersect_one's answer; it is what the cpu_baseline leg times.
+struct BuildRef { float lo[3], hi[3], c[3]; uint32_t prim; };
+
+static void grow(float* lo, float* hi, const float* l2, const float* h2) {
+  for (int a = 0; a < 3; ++a) { lo[a] = std::fmin(lo[a], l2[a]); hi[a] = std::fmax(hi[a], h2[a]); }
+}
+static float half_area(const float* lo, const float* hi) {
+  const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+static uint32_t build_node(const Scene& sc, std::vector<BuildRef>& refs, uint32_t b, uint32_t e) {
+  const uint32_t node = (uint32_t)sc.bvh.size();
+  sc.bvh.push_back(CpuBvhNode{});
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (uint32_t i = b; i < e; ++i) { grow(lo, hi, refs[i].lo, refs[i].hi); grow(clo, chi, refs[i].c, refs[i].c); }
+  for (int a = 0; a < 3; ++a) {   // outward padding: the slab test stays conservative under rounding
+    const float m = std::fmax(std::fabs(lo[a]), std::fabs(hi[a])), pad = 1e-5f * m + 1e-6f;
+    sc.bvh[node].lo[a] = lo[a] - pad;
+    sc.bvh[node].hi[a] = hi[a] + pad;
+  }
+  const uint32_t n = e - b;
+  auto make_leaf = [&]() {
+    sc.bvh[node].right_or_first = (uint32_t)sc.bvh_prims.size();
+    sc.bvh[node].count = n;
+    for (uint32_t i = b; i < e; ++i) sc.bvh_prims.push_back(refs[i].prim);
+    return node;
+  };
+  if (n <= 4) return make_leaf();
+  // 16-bin SAH on the centroid bounds' longest axis
+  int axis = 0;
+  for (int a = 1; a < 3; ++a) if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+  const float ext = chi[axis] - clo[axis];
+  if (!(ext > 0.0f)) return make_leaf();
+  constexpr int kBins = 16;
+  float blo[kBins][3], bhi[kBins][3];
+  uint32_t bcnt[kBins] = {};
+  for (int k = 0; k < kBins; ++k) for (int a = 0; a < 3; ++a) { blo[k][a] = INFINITY; bhi[k][a] = -INFINITY; }
+  auto bin_of = [&](const BuildRef& r) { return std::min(kBins - 1, (int)((r.c[axis] - clo[axis]) / ext * kBins)); };
+  for (uint32_t i = b; i < e; ++i) { const int k = bin_of(refs[i]); ++bcnt[k]; grow(blo[k], bhi[k], refs[i].lo, refs[i].hi); }
+  float best = INFINITY;
+  int split = -1;
+  for (int s = 1; s < kBins; ++s) {
+    float l0[3] = {INFINITY, INFINITY, INFINITY}, l1[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float r0[3] = {INFINITY, INFINITY, INFINITY}, r1[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t nl = 0, nr = 0;
+    for (int k = 0; k < s; ++k) if (bcnt[k]) { grow(l0, l1, blo[k], bhi[k]); nl += bcnt[k]; }
+    for (int k = s; k < kBins; ++k) if (bcnt[k]) { grow(r0, r1, blo[k], bhi[k]); nr += bcnt[k]; }
+    if (!nl || !nr) continue;
+    const float cost = half_area(l0, l1) * nl + half_area(r0, r1) * nr;
+    if (cost < best) { best = cost; split = s; }
+  }
+  uint32_t mid;
+  if (split < 0) {
+    mid = b + n / 2;
+  } else {
+    mid = (uint32_t)(std::partition(refs.begin() + b, refs.begin() + e,
+                                    [&](const BuildRef& r) { return bin_of(r) < split; }) - refs.begin());
+    if (mid == b || mid == e) mid = b + n / 2;
+  }
+  build_node(sc, refs, b, mid);   // left child = node + 1
+  const uint32_t right = build_node(sc, refs, mid, e);
+  sc.bvh[node].right_or_first = right;
+  sc.bvh[node].count = 0;
+  return node;
+}
+
+static void build_cpu_bvh(const Scene& sc) {
+  const size_t T = sc.references.size();
+  std::vector<BuildRef> refs(T);
+  for (size_t k = 0; k < T; ++k) {
+    BuildRef& r = refs[k];
+    r.prim = (uint32_t)k;
+    for (int a = 0; a < 3; ++a) { r.lo[a] = INFINITY; r.hi[a] = -INFINITY; }
+    for (int j = 0; j < 3; ++j) {
+      const float* v = sc.vertices[sc.references[k].tri[j]].v;
+      grow(r.lo, r.hi, v, v);
+    }
+    for (int a = 0; a < 3; ++a) r.c[a] = 0.5f * (r.lo[a] + r.hi[a]);
+  }
+  sc.bvh.reserve(T);
+  sc.bvh_prims.reserve(T);
+  if (T) build_node(sc, refs, 0, (uint32_t)T);
+}
+
+static inline float safe_inv(float d) { return 1.0f / (std::fabs(d) > 1e-20f ? d : std::copysign(1e-20f, d)); }
+
+static Intersection intersect_bvh(const Scene& sc, const float* o3, float tmin, const float* d3, float tmax) {
+  Intersection r{-1.0f, 0xFFFFFFFFu, {0.0f, 0.0f}};
+  if (tmax < 0.0f) return r;   // disabled ray (renderer/Shaders.metal:119,124,173)
+  std::call_once(sc.bvh_once, build_cpu_bvh, std::cref(sc));
+  if (sc.bvh.empty()) return r;
+  const F3 o = f3(o3), d = f3(d3);
+  const float inv[3] = {safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
+  const float oo[3] = {o.x, o.y, o.z};
+  bool found = false;
+  float bt = tmax, bu = 0, bv = 0;
+  uint32_t bk = 0;
+  auto box = [&](uint32_t n, float& tn) {
+    const CpuBvhNode& b = sc.bvh[n];
+    float t0 = tmin, t1 = bt;
+    for (int a = 0; a < 3; ++a) {
+      const float x0 = (b.lo[a] - oo[a]) * inv[a], x1 = (b.hi[a] - oo[a]) * inv[a];
+      t0 = std::fmax(t0, std::fmin(x0, x1));
+      t1 = std::fmin(t1, std::fmax(x0, x1));
+    }
+    tn = t0;
+    return t0 <= t1;
+  };
+  uint32_t stack[128];
+  int sp = 0;
+  uint32_t node = 0;
+  float tn0;
+  if (!box(0, tn0)) return r;
+  for (;;) {
+    const CpuBvhNode& nd = sc.bvh[node];
+    if (nd.count) {
+      for (uint32_t i = 0; i < nd.count; ++i) {
+        const uint32_t k = sc.bvh_prims[nd.right_or_first + i];
+        const uint32_t* tri = sc.references[k].tri;
+        float t, u, v;
+        if (!tri_hit(o, d, f3(sc.vertices[tri[0]].v), f3(sc.vertices[tri[1]].v), f3(sc.vertices[tri[2]].v),
+                     tmin, bt, t, u, v)) continue;
+        if (!found || t < bt || k < bk) { found = true; bt = t; bu = u; bv = v; bk = k; }
+      }
+    } else {
+      const uint32_t l = node + 1, rr = nd.right_or_first;
+      float tl, tr;
+      const bool hl = box(l, tl), hr = box(rr, tr);
+      if (hl && hr) {
+        const bool lf = tl <= tr;
+        stack[sp++] = lf ? rr : l;
+        node = lf ? l : rr;
+        continue;
+      }
+      if (hl || hr) { node = hl ? l : rr; continue; }
+    }
+    // pop (re-testing the box against the current nearest hit)
+    bool next = false;
+    while (sp > 0) {
+      node = stack[--sp];
+      float tn;
+      if (box(node, tn)) { next = true; break; }
+    }
+    if (!next) break;
   }
   if (found) { r.distance = bt; r.triangleIndex = bk; r.coordinates[0] = bu; r.coordinates[1] = bv; }
   return r;
@@ -603,7 +774,7 @@ static void rayGenerator(Ray& ray, unsigned x, unsigned y, unsigned W, unsigned 
 // intersectionHandler — Shaders.metal:105-212
 static void intersectionHandler(const Scene& sc, const Intersection& isect, Ray& ray, LightSamplingRay& sray,
                                 unsigned x, unsigned y, uint32_t frameIndex, uint32_t maxPathLength,
-                                const float* noiseTable) {
+                                const float* noiseTable, bool debugMaterial = false) {
   sray.maxDistance = -1.0f;                                                   // :119
   if (isect.distance < kDistanceEpsilon) { ray.maxDistance = -1.0f; return; } // :122-126
   const TriangleReference& ref = sc.references[isect.triangleIndex];          // :129
@@ -616,6 +787,10 @@ static void intersectionHandler(const Scene& sc, const Intersection& isect, Ray&
   Vertex hit = interpolate2(sc.vertices[ref.tri[0]], sc.vertices[ref.tri[1]], sc.vertices[ref.tri[2]],
                             isect.coordinates);                               // :140
   F3 hv = f3(hit.v), hn = f3(hit.n);
+  if (debugMaterial) {   // DEBUG_MATERIAL (Shaders.metal:7,142-147): radiance := Fresnel(n, -wI, 1, 1.5)
+    const float f = fresnel(hn, neg(wI), 1.0f, 1.5f);
+    for (int i = 0; i < 3; ++i) ray.radiance[i] = f;
+  }
   const LightTriangle* lts = sc.lightTriangles.data();
   if (bounce + 1 < maxPathLength) {                                           // :150-176
     const LightTriangle& lt = selectLightTriangle(noise[2], lts, (int)sc.lightTrianglesCount);
@@ -668,10 +843,11 @@ static void lightSamplingHandler(const Intersection& isect, Ray& ray, const Ligh
     for (int i = 0; i < 3; ++i) ray.radiance[i] += sray.throughput[i];
 }
 
-// accumulateImage — Shaders.metal:233-249
-static void accumulateImage(const Ray& ray, float* px, uint32_t frameIndex) {
+// accumulateImage — Shaders.metal:233-249 (accumulate = ACCUMULATE_IMAGE,
+// Raytracing.h:14: false writes the frame's radiance alone)
+static void accumulateImage(const Ray& ray, float* px, uint32_t frameIndex, bool accumulate = true) {
   float c[3] = {ray.radiance[0], ray.radiance[1], ray.radiance[2]};
-  if (frameIndex > 0) {
+  if (accumulate && frameIndex > 0) {
     float factor = float(frameIndex) / float(frameIndex + 1);
     for (int i = 0; i < 3; ++i) c[i] = mixf(c[i], px[i], factor);
   }
@@ -691,7 +867,9 @@ static int64_t noise_frame_for(int64_t f, unsigned i) {
 struct NoiseCache {
   uint64_t seed;
   std::vector<std::vector<float>> tables;   // index frame+1 (0 = initial table)
+  bool animate = true;                      // ANIMATE_NOISE (Raytracing.h:20); 0: the initial table for every frame
   const float* get(int64_t frame) {
+    if (!animate) frame = -1;   // Renderer.mm:485-497 skipped: the slots keep the table of :109-129
     size_t k = (size_t)(frame + 1);
     if (k >= tables.size()) tables.resize(k + 1);
     if (tables[k].empty()) { tables[k].resize(kNoiseDim * kNoiseDim * 4); noise_table(seed, frame, tables[k].data()); }
@@ -805,14 +983,15 @@ void orc_intersect(const orc_scene* sc, const void* rays, uint32_t stride, uint3
   }
 }
 
+// flags: ORC_DEBUG_MATERIAL (see orc_render)
 void orc_shade(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t frameIndex, uint32_t maxPathLength,
-               const float* noise, const void* isect, void* rays, void* srays) {
+               const float* noise, const void* isect, void* rays, void* srays, uint32_t flags) {
   const Intersection* is = (const Intersection*)isect;
   Ray* r = (Ray*)rays; LightSamplingRay* s = (LightSamplingRay*)srays;
   for (uint32_t y = 0; y < H; ++y)
     for (uint32_t x = 0; x < W; ++x) {
       uint32_t i = y * W + x;
-      intersectionHandler(sc->s, is[i], r[i], s[i], x, y, frameIndex, maxPathLength, noise);
+      intersectionHandler(sc->s, is[i], r[i], s[i], x, y, frameIndex, maxPathLength, noise, (flags & 4u) != 0);
     }
 }
 
@@ -822,9 +1001,20 @@ void orc_resolve(uint32_t count, const void* isect, void* rays, const void* sray
   for (uint32_t i = 0; i < count; ++i) lightSamplingHandler(is[i], r[i], s[i]);
 }
 
-void orc_accumulate(uint32_t count, uint32_t frameIndex, const void* rays, float* image_rgba) {
+// flags: ORC_NO_ACCUMULATE (see orc_render)
+void orc_accumulate(uint32_t count, uint32_t frameIndex, const void* rays, float* image_rgba, uint32_t flags) {
   const Ray* r = (const Ray*)rays;
-  for (uint32_t i = 0; i < count; ++i) accumulateImage(r[i], image_rgba + 4 * (size_t)i, frameIndex);
+  for (uint32_t i = 0; i < count; ++i) accumulateImage(r[i], image_rgba + 4 * (size_t)i, frameIndex, !(flags & 2u));
+}
+
+// intersect through the CPU baseline's BVH (same answers as orc_intersect)
+void orc_intersect_bvh(const orc_scene* sc, const void* rays, uint32_t stride, uint32_t count, void* isect_out) {
+  const uint8_t* p = (const uint8_t*)rays;
+  Intersection* out = (Intersection*)isect_out;
+  for (uint32_t i = 0; i < count; ++i) {
+    const float* f = (const float*)(p + (size_t)i * stride);
+    out[i] = intersect_bvh(sc->s, f, f[3], f + 4, f[7]);
+  }
 }
 
 // ---- whole-frame driver: performRaytracing: (renderer/Renderer.mm:500-585) --
@@ -835,12 +1025,23 @@ void orc_accumulate(uint32_t count, uint32_t frameIndex, const void* rays, float
 // active_out (optional) receives A = sum over iterations of rays alive at
 // the start of the iteration.  pixel_mask (optional, W*H bytes) restricts the
 // render to pixels with mask != 0 (others untouched) for bounded samples.
+// flags: the reference's compile-time switches (renderer/Raytracing.h:11-33,
+// renderer/Shaders.metal:7) and the traversal used —
+//   1 ORC_STATIC_NOISE     ANIMATE_NOISE 0: every frame reads the initial table
+//   2 ORC_NO_ACCUMULATE    ACCUMULATE_IMAGE false: the image is the last frame
+//   4 ORC_DEBUG_MATERIAL   DEBUG_MATERIAL 1: radiance := Fresnel at each hit
+//   8 ORC_BVH              nearest hits through the CPU BVH (the cpu_baseline
+//                          leg) instead of brute force — the same answers
 int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLength, uint64_t seed,
                uint32_t frame_begin, uint32_t frame_end, uint32_t threads, const uint8_t* pixel_mask,
-               float* image_rgba, uint64_t* active_out) {
+               float* image_rgba, uint64_t* active_out, uint32_t flags) {
   if (W < 2 || H < 2 || maxPathLength == 0) return -1;
-  const bool use_packets = sc->s.references.size() >= g_packet_threshold;
+  const bool use_bvh = (flags & 8u) != 0;
+  const bool use_packets = !use_bvh && sc->s.references.size() >= g_packet_threshold;
+  const bool debug_material = (flags & 4u) != 0, accumulate = (flags & 2u) == 0;
+  if (use_bvh) std::call_once(sc->s.bvh_once, build_cpu_bvh, std::cref(sc->s));
   NoiseCache nc{seed, {}};
+  nc.animate = (flags & 1u) == 0;
   std::atomic<uint64_t> active{0};
   if (threads == 0) threads = 1;
   for (uint32_t f = frame_begin; f < frame_end; ++f) {
@@ -878,11 +1079,12 @@ int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLeng
         for (uint32_t i = 0; i < maxPathLength; ++i) {
           for (size_t j = 0; j < n; ++j) local += rays[j].maxDistance >= 0.0f;
           trace(false);
-          for (size_t j = 0; j < n; ++j) intersectionHandler(sc->s, is[j], rays[j], srays[j], xs[j], y, f, maxPathLength, iterNoise[i]);
+          for (size_t j = 0; j < n; ++j)
+            intersectionHandler(sc->s, is[j], rays[j], srays[j], xs[j], y, f, maxPathLength, iterNoise[i], debug_material);
           trace(true);
           for (size_t j = 0; j < n; ++j) lightSamplingHandler(is[j], rays[j], srays[j]);
         }
-        for (size_t j = 0; j < n; ++j) accumulateImage(rays[j], image_rgba + 4 * ((size_t)y * W + xs[j]), f);
+        for (size_t j = 0; j < n; ++j) accumulateImage(rays[j], image_rgba + 4 * ((size_t)y * W + xs[j]), f, accumulate);
       }
       active += local;
     };
@@ -897,12 +1099,13 @@ int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLeng
           rayGenerator(ray, x, y, W, H, raygenNoise);
           for (uint32_t i = 0; i < maxPathLength; ++i) {
             if (ray.maxDistance >= 0.0f) ++local;
-            Intersection is = intersect_one(sc->s, ray.origin, ray.minDistance, ray.direction, ray.maxDistance);
-            intersectionHandler(sc->s, is, ray, sray, x, y, f, maxPathLength, iterNoise[i]);
-            Intersection is2 = intersect_one(sc->s, sray.origin, sray.minDistance, sray.direction, sray.maxDistance);
+            const auto isect = use_bvh ? intersect_bvh : intersect_one;
+            Intersection is = isect(sc->s, ray.origin, ray.minDistance, ray.direction, ray.maxDistance);
+            intersectionHandler(sc->s, is, ray, sray, x, y, f, maxPathLength, iterNoise[i], debug_material);
+            Intersection is2 = isect(sc->s, sray.origin, sray.minDistance, sray.direction, sray.maxDistance);
             lightSamplingHandler(is2, ray, sray);
           }
-          accumulateImage(ray, image_rgba + 4 * pix, f);
+          accumulateImage(ray, image_rgba + 4 * pix, f, accumulate);
         }
       active += local;
     };

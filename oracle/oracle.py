@@ -53,6 +53,14 @@ LIGHT_DTYPE = np.dtype({
 
 _lib = None
 
+# orc_render / orc_shade / orc_accumulate flags: the reference's compile-time
+# switches (renderer/Raytracing.h:14,20; renderer/Shaders.metal:7) and the
+# traversal the CPU baseline times
+STATIC_NOISE = 1      # ANIMATE_NOISE 0
+NO_ACCUMULATE = 2     # ACCUMULATE_IMAGE false
+DEBUG_MATERIAL = 4    # DEBUG_MATERIAL 1
+BVH = 8               # nearest hits through the CPU BVH (same answers as brute force)
+
 
 def build() -> None:
     """Compile the oracle with its committed Makefile (gcc, -ffp-contract=off)."""
@@ -79,10 +87,11 @@ def lib() -> ctypes.CDLL:
         L.orc_noise_frame_for.restype = i64
         L.orc_raygen.argtypes = [u32, u32, vp, vp]
         L.orc_intersect.argtypes = [vp, vp, u32, u32, vp]
-        L.orc_shade.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp]
+        L.orc_intersect_bvh.argtypes = [vp, vp, u32, u32, vp]
+        L.orc_shade.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, u32]
         L.orc_resolve.argtypes = [u32, vp, vp, vp]
-        L.orc_accumulate.argtypes = [u32, u32, vp, vp]
-        L.orc_render.argtypes = [vp, u32, u32, u32, u64, u32, u32, u32, vp, vp, vp]
+        L.orc_accumulate.argtypes = [u32, u32, vp, vp, u32]
+        L.orc_render.argtypes = [vp, u32, u32, u32, u64, u32, u32, u32, vp, vp, vp, u32]
         L.orc_set_packet_threshold.argtypes = [u64]
         _lib = L
     return _lib
@@ -145,17 +154,25 @@ class OracleScene:
         lib().orc_intersect(self.h, _p(rays), rays.dtype.itemsize, len(rays), _p(out))
         return out
 
-    def shade(self, W, H, frame_index, max_path_length, noise, isect, rays, srays):
-        lib().orc_shade(self.h, W, H, frame_index, max_path_length, _p(noise), _p(isect), _p(rays), _p(srays))
+    def intersect_bvh(self, rays: np.ndarray) -> np.ndarray:
+        """intersect() through the CPU baseline's BVH (identical answers)."""
+        rays = np.ascontiguousarray(rays)
+        out = np.zeros(len(rays), ISECT_DTYPE)
+        lib().orc_intersect_bvh(self.h, _p(rays), rays.dtype.itemsize, len(rays), _p(out))
+        return out
 
-    def render(self, W, H, L, seed, frames, frame_begin=0, threads=1, image=None, pixel_mask=None):
-        """Returns (image[H,W,4] float32, active ray-bounces A)."""
+    def shade(self, W, H, frame_index, max_path_length, noise, isect, rays, srays, flags=0):
+        lib().orc_shade(self.h, W, H, frame_index, max_path_length, _p(noise), _p(isect), _p(rays), _p(srays), flags)
+
+    def render(self, W, H, L, seed, frames, frame_begin=0, threads=1, image=None, pixel_mask=None, flags=0):
+        """Returns (image[H,W,4] float32, active ray-bounces A); flags: STATIC_NOISE,
+        NO_ACCUMULATE, DEBUG_MATERIAL, BVH."""
         if image is None:
             image = np.zeros((H, W, 4), np.float32)
         active = np.zeros(1, np.uint64)
         mask_p = _p(pixel_mask) if pixel_mask is not None else None
         rc = lib().orc_render(self.h, W, H, L, seed, frame_begin, frame_begin + frames, threads, mask_p,
-                              _p(image), _p(active))
+                              _p(image), _p(active), flags)
         if rc != 0:
             raise RuntimeError("orc_render failed")
         return image, int(active[0])
@@ -191,8 +208,8 @@ def resolve(isect, rays, srays):
     lib().orc_resolve(len(rays), _p(isect), _p(rays), _p(srays))
 
 
-def accumulate(frame_index, rays, image):
-    lib().orc_accumulate(len(rays), frame_index, _p(rays), _p(image))
+def accumulate(frame_index, rays, image, flags=0):
+    lib().orc_accumulate(len(rays), frame_index, _p(rays), _p(image), flags)
 
 
 def to_srgb(v: np.ndarray) -> np.ndarray:

@@ -342,3 +342,53 @@ def test_golden_compare_display(gpu, mrt_mod, oracle_mod):
         finally:
             r2.close()
     r.close()
+
+
+@pytest.mark.parametrize("switch", ["static_noise", "no_accumulate", "debug_material", "all"])
+@pytest.mark.parametrize("scene,L", [("cornellbox", 4), ("CornellBox-Water-plastic", 8)])
+def test_compile_time_switches_match_oracle(gpu, mrt_mod, oracle_mod, switch, scene, L):
+    """The reference's compile-time switches as runtime flags, precise build
+    vs the oracle bitwise: ANIMATE_NOISE 0 (Raytracing.h:20, Renderer.mm:
+    485-497), ACCUMULATE_IMAGE false (Raytracing.h:14, Shaders.metal:241),
+    DEBUG_MATERIAL 1 (Shaders.metal:7,142-147) — over two draws so the
+    running mean, frame batches and noise window all take part."""
+    W, H, frames = 72, 40, (3, 2)
+    on = {k: switch in (k, "all") for k in ("static_noise", "no_accumulate", "debug_material")}
+    oflags = ((oracle_mod.STATIC_NOISE if on["static_noise"] else 0) |
+              (oracle_mod.NO_ACCUMULATE if on["no_accumulate"] else 0) |
+              (oracle_mod.DEBUG_MATERIAL if on["debug_material"] else 0))
+    sc, osc = _scene(mrt_mod, scene), _oscene(oracle_mod, mrt_mod, scene)
+    ref, A = osc.render(W, H, L, SEED, sum(frames), threads=8, flags=oflags)
+    r = mrt_mod.Renderer(sc, W, H, L, precise=True, animate_noise=not on["static_noise"],
+                         accumulate_image=not on["no_accumulate"], debug_material=on["debug_material"])
+    for n in frames:
+        r.draw(n)
+    img, st = r.read_image(), r.stats()
+    r.close()
+    plain, _ = osc.render(W, H, L, SEED, sum(frames), threads=8)
+    assert img.tobytes() != plain.tobytes()          # the switch changes the image
+    rel, rmse, same = pixel_metrics(img, ref)
+    print(f"{switch} {scene}: bit-identical {same:.5f}")
+    assert np.mean(rel <= 1e-4) >= 0.999 and rmse <= 1e-3
+    assert st["active_ray_bounces"] == A
+
+
+def test_debug_material_stage_and_no_accumulate_stage(gpu, mrt_mod, oracle_mod):
+    """mrt_shade with MRT_FLAG_DEBUG_MATERIAL and mrt_accumulate with
+    MRT_FLAG_NO_ACCUMULATE (the stage ABI, B-2) equal the oracle's stages."""
+    W, H, L, f = 40, 30, 4, 5
+    sc, osc = _scene(mrt_mod, "CornellBox-Water-plastic"), _oscene(oracle_mod, mrt_mod, "CornellBox-Water-plastic")
+    rays = oracle_mod.raygen(W, H, oracle_mod.noise_table(SEED, f))
+    noise = oracle_mod.noise_table(SEED, oracle_mod.noise_frame_for(f, 0))
+    isect = osc.intersect(rays)
+    srays = np.zeros(W * H, oracle_mod.SRAY_DTYPE)
+    d_rays, d_srays, d_isect, d_noise = to_dev(rays), to_dev(srays), to_dev(isect), to_dev(noise)
+    osc.shade(W, H, f, L, noise, isect, rays, srays, oracle_mod.DEBUG_MATERIAL)
+    mrt_mod.shade(sc, W, H, f, L, dev_ptr(d_noise), dev_ptr(d_isect), dev_ptr(d_rays), dev_ptr(d_srays),
+                  debug_material=True)
+    assert from_dev(d_rays, oracle_mod.RAY_DTYPE).tobytes() == rays.tobytes()
+    img = np.full((H, W, 4), 0.25, np.float32)
+    d_img = to_dev(img)
+    oracle_mod.accumulate(7, rays, img, oracle_mod.NO_ACCUMULATE)
+    mrt_mod.accumulate(sc, W, H, 7, dev_ptr(d_rays), dev_ptr(d_img), accumulate_image=False)
+    assert from_dev(d_img, np.float32).tobytes() == img.tobytes()

@@ -192,7 +192,7 @@ def _fresnel64(cos_i, eta_out, eta_in):
     return 0.5 * (rs * rs + rp * rp)
 
 
-def _shade_one(oracle_mod, mtype, ior, noise4, current_ior=1.00029):
+def _shade_one(oracle_mod, mtype, ior, noise4, current_ior=1.00029, flags=0, L=4):
     V = np.zeros(6, oracle_mod.VERTEX_DTYPE)
     V["v"] = [(1, 0, 0), (1, 0, -1), (0, 0, 0), (-1, 2, -1), (1, 2, -1), (0, 2, 1)]
     V["n"] = [(0, 1, 0)] * 3 + [(0, -1, 0)] * 3
@@ -216,7 +216,7 @@ def _shade_one(oracle_mod, mtype, ior, noise4, current_ior=1.00029):
     isect["coordinates"] = (1.0, 0.0)          # the hit is V0 = (1, 0, 0), n = (0, 1, 0)
     srays = np.zeros(1, oracle_mod.SRAY_DTYPE)
     noise = np.tile(np.float32(noise4), 64 * 64)
-    sc.shade(1, 1, 0, 4, noise, isect, ray, srays)
+    sc.shade(1, 1, 0, L, noise, isect, ray, srays, flags)
     return ray[0], srays[0], d.astype(np.float64)
 
 
@@ -271,3 +271,69 @@ def test_diffuse_bsdf_known_answer(oracle_mod):
     np.testing.assert_allclose(ray["direction"], [np.cos(phi) * 0.6, cos_t, -np.sin(phi) * 0.6], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(ray["throughput"], _KD, rtol=1e-6)
     np.testing.assert_allclose(ray["params"], [cos_t / _PI_REF, 1.0, 2.0, 1.00029], rtol=1e-6)
+
+
+# ------------------------------------------------- CPU baseline traversal (BVH)
+@pytest.mark.parametrize("scene", ["cornellbox", "CornellBox-Water-plastic", "procedural"])
+def test_cpu_bvh_equals_bruteforce(oracle_mod, mrt_mod, scene):
+    """The cpu_baseline leg's BVH traversal ("same BVH") gives
+    the brute-force nearest hit bit for bit — random rays incl. disabled,
+    axis-parallel and on-surface starts — and the same rendered image and A."""
+    if scene == "procedural":
+        e = mrt_mod.Scene("cornellbox", procedural_triangles=8192, procedural_seed=5, device=-1).export()
+        sc = oracle_mod.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
+    else:
+        sc = oracle_mod.OracleScene(mrt_mod.scene_path(scene))
+    rng = np.random.default_rng(11)
+    n = 4000
+    r = np.zeros(n, oracle_mod.RAY_DTYPE)
+    r["origin"] = rng.uniform([-0.95, 0.05, -0.95], [0.95, 1.95, 2.3], size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    r["direction"] = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    r["maxDistance"] = np.float32(np.inf)
+    r["maxDistance"][::17] = -1.0
+    r["maxDistance"][5::23] = rng.uniform(0.01, 1.0, size=len(r["maxDistance"][5::23]))
+    r["direction"][1::31] = np.array([0.0, 1.0, 0.0], np.float32)
+    r["direction"][2::31] = np.array([0.0, 0.0, -1.0], np.float32)
+    r["origin"][3::37, 1] = 0.0
+    assert sc.intersect_bvh(r).tobytes() == sc.intersect(r).tobytes()
+    a, A = sc.render(48, 36, 4, SEED, 2, threads=4)
+    b, B = sc.render(48, 36, 4, SEED, 2, threads=4, flags=oracle_mod.BVH)
+    assert a.tobytes() == b.tobytes() and A == B
+
+
+# ------------------------------- compile-time switches (Raytracing.h, Shaders.metal)
+def test_static_noise_reads_the_initial_table(oracle_mod, cornell):
+    """ANIMATE_NOISE 0 (Raytracing.h:20, Renderer.mm:485-497): every frame and
+    iteration reads the initial table, so with ACCUMULATE_IMAGE off frames
+    f and f' whose (f/3, f/5) agree render identical images (the noise cell
+    of Shaders.metal:135-136 depends on the frame only through f/3 and f/5)."""
+    S, N = oracle_mod.STATIC_NOISE, oracle_mod.NO_ACCUMULATE
+    a, _ = cornell.render(32, 24, 4, SEED, 1, frame_begin=0, flags=S | N)
+    b, _ = cornell.render(32, 24, 4, SEED, 1, frame_begin=1, flags=S | N)   # 1/3 = 0, 1/5 = 0
+    c, _ = cornell.render(32, 24, 4, SEED, 1, frame_begin=1, flags=N)       # animated: another table
+    assert a.tobytes() == b.tobytes()
+    assert a.tobytes() != c.tobytes()
+
+
+def test_no_accumulate_keeps_the_last_frame(oracle_mod, cornell):
+    """ACCUMULATE_IMAGE false (Raytracing.h:14, Shaders.metal:241): the image
+    after frames 0..k is frame k's radiance alone, alpha 1."""
+    N = oracle_mod.NO_ACCUMULATE
+    img, _ = cornell.render(32, 24, 3, SEED, 4, flags=N)
+    last, _ = cornell.render(32, 24, 3, SEED, 1, frame_begin=3, flags=N)
+    mean, _ = cornell.render(32, 24, 3, SEED, 4)
+    assert img.tobytes() == last.tobytes() and np.all(img[..., 3] == 1.0)
+    assert img.tobytes() != mean.tobytes()
+
+
+def test_debug_material_known_answer(oracle_mod):
+    """DEBUG_MATERIAL 1 (Shaders.metal:7,142-147): at each hit the radiance is
+    SET to fresnel(n, -wI, 1.0, 1.5) before emission and NEE add to it; a
+    primary ray at 45 degrees onto a non-emissive floor, L = 1 (no NEE):
+    radiance = the unpolarised Fresnel reflectance at 45 degrees, 1.0 -> 1.5."""
+    ray, d, _ = _shade_one(oracle_mod, 0, 0.0, [0.5, 0.5, 0.5, 0.5], flags=oracle_mod.DEBUG_MATERIAL, L=1)
+    want = _fresnel64(np.cos(np.pi / 4), 1.0, 1.5)
+    assert np.allclose(ray["radiance"], want, rtol=1e-5, atol=0) and ray["radiance"][0] == ray["radiance"][2]
+    ray0, _, _ = _shade_one(oracle_mod, 0, 0.0, [0.5, 0.5, 0.5, 0.5], L=1)
+    assert np.all(ray0["radiance"] == 0.0)
