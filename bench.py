@@ -13,7 +13,11 @@ torch is used only as the CPU control plane for N > 1 (gloo: the RCCL unique
 id broadcast, barriers and the max over ranks); no torch GPU state exists.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c3g|c4|c5]
-For N > 1 launch with torch.distributed.run (one process per GPU).
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) each
+process is one rank; without it, bench.py starts the N ranks itself (children
+with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, before any HIP call),
+prints rank 0's line and fails if any rank fails.  --sweep-gpus 1,2,4,8 runs
+one such job per N and prints one line each (e.g. --config c5 on one node).
 --shard-of S (N = 1 only): render only rank 0's tiles of an S-way split —
 one GPU's share of a multi-GPU job, value = that share's paths/s (diagnostic).
 """
@@ -30,6 +34,10 @@ sys.path.insert(0, os.path.join(ROOT, "metal-renderer_amd"))
 
 METRIC = "Mpaths/s at 1920×1080, 4 bounces; achieved HBM GB/s vs peak; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue roof: 256 CUs x 4 SIMDs, a wave64 VALU instruction issues over 2
+# cycles (32 lanes/cycle per SIMD, MI355X_MICROARCH.md), at the 2.4-GHz peak
+# engine clock = 78.6 T lane-ops/s (the FP32 vector peak 157.3 TFLOP/s / 2)
+VALU_PEAK_TLANE = 1024 * 32 * 2.4e9 / 1e12
 B_PATH, B_BOUNCE = 112, 312    # algorithmic bytes per path / per active ray-bounce
 
 CONFIGS = {
@@ -72,7 +80,7 @@ def parse():
                    help="BVH builder: host binned SAH (default), device LBVH or device PLOC")
     p.add_argument("--cpu-frames", type=int, default=0,
                    help="frames of the workload timed on the CPU oracle (default: all spp frames for C2, 8 otherwise)")
-    p.add_argument("--pmc", default=None, help="JSON with PMC HBM traffic per bounce launch (profiles/)")
+    p.add_argument("--pmc", default=None, help="JSON with the PMC counts per hot-kernel launch (profiles/pmc_<config>.json)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="N=1 only: time rank 0's tiles of an S-way tile split (one GPU's share)")
     p.add_argument("--shard-rank", type=int, default=0,
@@ -88,7 +96,72 @@ def parse():
     p.add_argument("--exchange-backend", default="rccl", choices=["rccl", "host"],
                    help="rccl: libmrt's RCCL collective (one process per GPU); host: packed tiles through host "
                         "memory and a gloo gather (rehearsal of the N>1 path with several ranks on one GPU)")
+    p.add_argument("--sweep-gpus", default="",
+                   help="comma-separated GPU counts (e.g. 1,2,4,8): one job per N, one JSON line each")
+    p.add_argument("--rank-timeout", type=float, default=1800.0,
+                   help="self-launched ranks: seconds before a job whose ranks have not all exited is killed")
     return p.parse_args()
+
+
+def _child_argv(n):
+    """This command line for a self-launched job of n ranks (--gpus n, no sweep)."""
+    out, skip = [], False
+    for a in sys.argv[1:]:
+        if skip:
+            skip = False
+            continue
+        if a in ("--gpus", "--sweep-gpus"):
+            skip = True
+            continue
+        if a.startswith("--gpus=") or a.startswith("--sweep-gpus="):
+            continue
+        out.append(a)
+    return [sys.executable, os.path.abspath(__file__)] + out + ["--gpus", str(n)]
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args):
+    """Start each job's ranks as child processes (this process never touches
+    the GPU); rank 0 prints the JSON line.  Returns the first non-zero exit
+    status, after stopping the job's other ranks."""
+    import subprocess
+    counts = [int(x) for x in args.sweep_gpus.split(",") if x.strip()] if args.sweep_gpus else [args.gpus]
+    for n in counts:
+        port = _free_port()
+        procs = []
+        for rank in range(n):
+            env = dict(os.environ)
+            if n > 1:
+                env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                           GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen(_child_argv(n), env=env))
+        t_end = time.time() + args.rank_timeout
+        failed = 0
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad or time.time() > t_end:
+                failed = bad[0] if bad else 124
+                for p in procs:   # the ranks this process started (exact PIDs)
+                    if p.poll() is None:
+                        p.terminate()
+                for p in procs:
+                    try:
+                        p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                break
+            time.sleep(0.2)
+        failed = failed or next((p.returncode for p in procs if p.returncode), 0)
+        if failed:
+            print(f"bench.py: a rank of the {n}-GPU job failed (exit {failed})", file=sys.stderr, flush=True)
+            return failed
+    return 0
 
 
 def resolve_mtl(cfg):
@@ -138,12 +211,14 @@ def host_threads():
 
 
 def cpu_baseline(cfg, frames):
-    """The CPU oracle (scalar C++ restatement of the path, oracle/; brute-force
-    nearest hit in place of MPS) timed on this host on a bounded sample of the
-    same workload: C2 runs in full (all `frames` = spp frames
-    of the whole image) on every CPU of the process's share, and 2 frames on
-    one thread give the scalar rate.  Scenes with more triangles run one frame
-    of a row band sized to ~10 s on all threads and ~10 s on one.
+    """The CPU oracle (scalar C++ restatement of the path, oracle/) timed on
+    this host on a bounded sample of the same workload, its
+    nearest hits through a binned-SAH BVH (oracle ORC_BVH: the same answers
+    as its brute force, tests/test_oracle.py) — "same BVH", not brute force.
+    C2 runs in full (all `frames` = spp frames of the whole image) on every
+    CPU of the process's share, and 2 frames on one thread give the scalar
+    rate.  Other scenes run one frame of a row band sized from a pilot band to
+    ~10 s on all threads and ~10 s on one.
     Returns (baseline dict, oracle image, pixel mask, frames) — the image is
     kept for the parity check of the GPU render (main)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -161,41 +236,48 @@ def cpu_baseline(cfg, frames):
     else:
         sc = oracle.OracleScene(mrt.scene_path(cfg["scene"]), resolve_mtl(cfg))
     W, H = cfg["width"], cfg["height"]
+    B = oracle.BVH
     if sc.n_triangles <= 64:
         rows = H                      # C2: the whole workload (all spp frames)
         rows1 = H
         f1 = min(2, frames)
     else:
-        # brute force costs ~ (bounces x 2 traversals x triangles) tests per
-        # path at ~1.6e8 tests/s per thread (per-ray form) or ~5e8 (packet
-        # form, scenes >= oracle.PACKET_THRESHOLD triangles): size the sample
-        # to ~10 s on all threads (one frame of a row band) and ~10 s on one
+        # one frame of a row band: a pilot band of 8 rows on all threads (it
+        # also builds the BVH) gives the rate; the band is sized to ~10 s on
+        # all threads and ~10 s on one
         frames = 1
-        rate = 5e8 if sc.n_triangles >= oracle.PACKET_THRESHOLD else 1.6e8
-        per_path = min(cfg["L"], 5) * 2 * sc.n_triangles
-        rows = max(1, min(H, int(10.0 * rate * threads / (per_path * W))))
-        rows1 = max(1, rows // threads)
+        pilot = np.zeros((H, W), np.uint8)
+        pilot[(H - 8) // 2:(H - 8) // 2 + 8] = 1
+        sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, 1, threads=threads, pixel_mask=pilot, flags=B)   # BVH build
+        tp = time.perf_counter()
+        sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, 1, threads=threads, pixel_mask=pilot, flags=B)
+        per_row = max(1e-6, (time.perf_counter() - tp) / 8)
+        rows = max(1, min(H, int(10.0 / per_row)))
+        rows1 = max(1, min(H, int(10.0 / (per_row * threads))))
         f1 = 1
     mask = np.zeros((H, W), np.uint8)
     y0 = (H - rows) // 2
     mask[y0:y0 + rows] = 1
     t0 = time.perf_counter()
-    img, _ = sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads, pixel_mask=mask)
+    img, _ = sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, frames, threads=threads, pixel_mask=mask, flags=B)
     dt = time.perf_counter() - t0
     paths = W * rows * frames
     mask1 = np.zeros((H, W), np.uint8)
-    mask1[y0:y0 + rows1] = 1
+    y1 = (H - rows1) // 2
+    mask1[y1:y1 + rows1] = 1
     t1 = time.perf_counter()
-    sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, f1, threads=1, pixel_mask=mask1)
+    sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, f1, threads=1, pixel_mask=mask1, flags=B)
     dt1 = time.perf_counter() - t1
     base = {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
             "single_thread_value": round(W * rows1 * f1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
             "cpu_model": _cpu_model(),
             "sample": f"frames 0-{frames - 1}, rows {y0}-{y0 + rows - 1} of the workload ({W}x{rows} of {W}x{H}, "
-                      f"L={cfg['L']}, {paths} paths), brute-force nearest hit over {sc.n_triangles} triangles, "
-                      f"{threads} std::threads over rows (the process's CPU share: affinity "
-                      f"{len(os.sched_getaffinity(0))}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS', '-')}), "
-                      f"{dt:.2f} s wall; single thread: frames 0-{f1 - 1} of rows {y0}-{y0 + rows1 - 1}, {dt1:.2f} s"}
+                      f"L={cfg['L']}, {paths} paths), nearest hits through a binned-SAH BVH over "
+                      f"{sc.n_triangles} triangles (same answers as brute force), "
+                      f"{threads} std::threads over rows = the process's CPU share (affinity "
+                      f"{len(os.sched_getaffinity(0))} of {os.cpu_count()} host CPUs, OMP_NUM_THREADS "
+                      f"{os.environ.get('OMP_NUM_THREADS', '-')}), {dt:.2f} s wall; single thread: frames "
+                      f"0-{f1 - 1} of rows {y1}-{y1 + rows1 - 1}, {dt1:.2f} s"}
     return base, img, mask, frames
 
 
@@ -221,8 +303,64 @@ def image_parity(gpu_img, ref_img, mask, build, frames, note):
             "note": note}
 
 
+def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_step):
+    """The hot kernel against its physical roofs, from the PMC passes of the
+    same command (tools/profile.sh -> tools/prof_summary.py ->
+    profiles/pmc_<config>.json; rocprofv3 --pmc has to wrap the process, so
+    the counts come from that file, recorded with the md5 of the libmrt.so
+    it measured) divided by this run's HIP-event launch time:
+      hbm  — (2 x FETCH_SIZE + WRITE_SIZE) bytes per launch (MI355X_MICROARCH.md
+             gfx950 correction) / launch time, against 8 TB/s;
+      valu — SQ_INSTS_VALU x 64 lane-slots per launch / launch time, against
+             1024 SIMDs x 32 lanes/cycle x 2.4 GHz (a wave64 VALU instruction
+             holds its SIMD's issue for 2 cycles whatever its exec mask).
+    bound = the roof with the larger fraction (the counter-measured limiter);
+    *_vs_step = the same counts per step over ms_per_step (<= frac: the check
+    against the wall clock)."""
+    import mrt
+    out = {"bound": "unmeasured", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    if not (os.path.exists(pmc_path) and not args.precise and (args.pmc or whole_frame) and timed):
+        out["note"] = ("no PMC passes for this command in profiles/ (they measure the whole frame of the fast "
+                       "build on one GPU)")
+        return out
+    with open(pmc_path) as f:
+        pmc = json.load(f)
+    traffic = pmc.get("hbm_bytes_per_launch")
+    valu_insts = (pmc.get("sq") or {}).get("SQ_INSTS_VALU")
+    roofs = {}
+    if traffic:
+        gbs = traffic / launch_s / 1e9
+        roofs["hbm"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "frac_vs_step": round(traffic * launches_per_step / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                        "bytes_per_launch": traffic}
+    if valu_insts:
+        t = valu_insts * 64 / launch_s / 1e12
+        roofs["valu-issue"] = {"achieved": round(t, 2), "peak": round(VALU_PEAK_TLANE, 2),
+                               "unit": "T VALU lane-slots/s", "frac": round(t / VALU_PEAK_TLANE, 4),
+                               "frac_vs_step": round(valu_insts * 64 * launches_per_step / step_s / 1e12
+                                                     / VALU_PEAK_TLANE, 4),
+                               "wave_instructions_per_launch": valu_insts}
+    if not roofs:
+        out["note"] = f"{os.path.basename(pmc_path)} holds no counts"
+        return out
+    bound = max(roofs, key=lambda k: roofs[k]["frac"])
+    out.update({k: roofs[bound][k] for k in ("achieved", "peak", "unit", "frac", "frac_vs_step")})
+    out.update({"bound": bound, "traffic": traffic, "roofs": roofs,
+                "wait_any_frac": pmc.get("wait_any_frac"),
+                "pmc_clock_ghz": pmc.get("clock_ghz"),
+                "rocprof_avg_launch_ms": round(pmc["avg_launch_ns_rocprof"] / 1e6, 4)
+                if pmc.get("avg_launch_ns_rocprof") else None,
+                "source": f"profiles/{os.path.basename(pmc_path)} (tag {pmc.get('tag')}, commit "
+                          f"{pmc.get('commit', 'unrecorded')}, lib md5 {pmc.get('lib_md5')})",
+                "same_library": (pmc.get("lib_md5") == lib_md5(mrt.LIB_PATH)) if pmc.get("lib_md5") else None})
+    return out
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.sweep_gpus):
+        sys.exit(launch(args))   # N ranks started here, before any HIP call
     cfg = CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -330,14 +468,10 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_paths / elapsed / 1e6
 
-    # roofline of the dominant kernel (the fused bounce kernel: every launch of
-    # the frame is one) from HIP events recorded around the launches of every
-    # 8th frame on the stream they run on, over the timed steps of this rank
-    # (timing events serialise a stream, so timing every launch would cost
-    # 3-20 %).  With frames in flight the launches overlap, so two rates:
-    #   achieved      = algorithmic bytes per launch / average launch duration
-    #                   (the definition rocprofv3's per-dispatch average checks)
-    #   achieved_job  = algorithmic bytes of the timed steps / their wall time
+    # Roofline of the dominant kernel (stream_kernel on C1/C2, path_kernel on
+    # C3-C5: one launch per frame batch), its launch time measured live with
+    # HIP events on the renderer's stream around every 8th batch's launch
+    # (timing events serialise a stream, so not every launch is timed).
     A = st["active_ray_bounces"] - base["active_ray_bounces"]
     P = st["paths"] - base["paths"]
     launches = st["kernel_launches"] - base["kernel_launches"]
@@ -345,32 +479,27 @@ def main():
     kms = st["kernel_ms"] - base["kernel_ms"]
     bytes_alg = B_PATH * P + B_BOUNCE * A
     avg_launch_ms = kms / max(1, timed)
-    achieved = (bytes_alg / max(1, launches)) / (avg_launch_ms * 1e-3) / 1e9 if timed else 0.0
-    achieved_job = bytes_alg / elapsed / 1e9
-    # PMC-measured figures of the same command (tools/profile.sh ->
-    # tools/prof_summary.py -> profiles/pmc_<config>.json, which records the
-    # commit it was taken at): HBM (fabric) bytes per launch and the VALU
-    # issue share.  rocprofv3 --pmc has to wrap the process, so they cannot
-    # come from this run; "source" says where they did come from.
-    traffic, counter = None, None
-    # (the committed passes measured the whole frame on one GPU: not a tile
-    # share's launches, so they are used only for that geometry)
-    pmc_path = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-    whole_frame = shard_count == 1 and not args.max_path_length
-    if os.path.exists(pmc_path) and not args.precise and (args.pmc or whole_frame):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        traffic = pmc.get("hbm_bytes_per_launch")
-        if traffic and timed:
-            gbs = traffic / (avg_launch_ms * 1e-3) / 1e9
-            counter = {"hbm_bytes_per_launch": traffic, "hbm_gbs": round(gbs, 1),
-                       "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
-                       "traffic_over_alg_bytes": round(traffic / max(1, bytes_alg / max(1, launches)), 3),
-                       "valu_issue_frac": pmc.get("valu_issue_frac"), "wait_frac": pmc.get("wait_any_frac"),
-                       "source": f"profiles/{os.path.basename(pmc_path)} (tag {pmc.get('tag')}, "
-                                 f"commit {pmc.get('commit', 'unrecorded')})",
-                       # the PMC passes measured this very library build (md5 of lib/libmrt.so)
-                       "same_library": (pmc.get("lib_md5") == lib_md5(mrt.LIB_PATH)) if pmc.get("lib_md5") else None}
+    launch_s = avg_launch_ms * 1e-3
+    launches_per_step = launches / max(1, args.steps)
+    roof = roofline(args, pmc_path=args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json"),
+                    whole_frame=shard_count == 1 and not args.max_path_length, timed=timed, launch_s=launch_s,
+                    step_s=ms_per_step * 1e-3, launches_per_step=launches_per_step)
+    # the reference's wavefront data contract (112 B per path +
+    # 312 B per active ray-bounce) per launch / launch time: an EQUIVALENT
+    # bandwidth — the bytes the reference's 2 + 4L passes would move, not
+    # bytes this fused kernel moves (it keeps hits and shadow rays in
+    # registers), so it can exceed the HBM peak and is not the roofline
+    alg = (bytes_alg / max(1, launches)) / launch_s / 1e9 if timed else 0.0
+    roof.update({
+        "alg_equiv_gbs": round(alg, 1), "alg_equiv_frac": round(alg / HBM_PEAK_GBS, 4),
+        "alg_equiv_note": "SURVEY 8(d) algorithmic bytes (the reference's 2+4L-pass AoS traffic) per launch / "
+                          "launch time: the bytes the reference's wavefront would move, not this kernel's",
+        "kernel": {1: "path_kernel (all bounces per launch)",
+                   2: "stream_kernel (wave-local streaming wavefront: all bounces per launch)"}.get(
+                       st["kernel"], "bounce_kernel (one launch per bounce)"),
+        "launches": launches, "timed_launches": timed, "avg_launch_ms": round(avg_launch_ms, 4),
+        "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
+        "active_ray_bounces_per_step": int(A / max(1, args.steps))})
 
     result = {
         "metric": METRIC,
@@ -398,27 +527,7 @@ def main():
                    "bvh": {"builder": {"sah": "host-sah", "lbvh": "device-lbvh", "ploc": "device-ploc"}[args.bvh],
                            "build_ms": round(scene.info["build_ms"], 2), "nodes": scene.info["bvh_nodes"],
                            "max_stack": scene.info["bvh_max_stack"]}},
-        # achieved / frac: ALGORITHMIC bytes (112 B per path + 312 B
-        # per active ray-bounce, the reference's wavefront data contract) per
-        # launch / HIP-event launch time — an equivalent bandwidth, not the
-        # bytes the fused kernel moves; "counter" holds the PMC-measured HBM
-        # rate (far lower: hits and shadow rays stay in registers) and the VALU
-        # issue share, which is what actually bounds the kernel
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "achieved_is": "algorithmic bytes per launch / launch time (equivalent bandwidth)",
-                     "frac_note": "SURVEY 8(d) algorithmic bytes (the reference's 2+4L-pass wavefront traffic); "
-                                  "the fused kernel moves far fewer, so frac can exceed 1 - counter.hbm_frac is the "
-                                  "measured HBM rate",
-                     "counter": counter,
-                     "limiter": "VALU issue + memory latency of BVH traversal (not HBM bandwidth)",
-                     "achieved_job": round(achieved_job, 1), "frac_job": round(achieved_job / HBM_PEAK_GBS, 4),
-                     "kernel": {1: "path_kernel (all bounces per launch)", 2: "stream_kernel (wave-local streaming wavefront: all bounces per launch)"}.get(
-                         st["kernel"], "bounce_kernel (one launch per bounce)"),
-                     "launches": launches, "timed_launches": timed,
-                     "avg_launch_ms": round(avg_launch_ms, 4),
-                     "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
-                     "active_ray_bounces_per_step": int(A / max(1, args.steps))},
+        "roofline": roof,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:

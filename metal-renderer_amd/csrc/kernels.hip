@@ -1364,7 +1364,13 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
     const uint32_t idx = first + lane;                                  // camera: the launch's dense index
     const uint32_t slot = qbase + (lvl - 1u) * kStreamCap + first + lane;   // level lvl >= 1: the queue slot
     const uint32_t out = lvl + 1u < L ? qbase + lvl * kStreamCap + cnt[lvl + 1u] : 0u;
-    // the wave reads rays its own lanes wrote: their stores first
+    // The wave reads rays its own lanes wrote: their stores first.  This
+    // relies on gfx9 (CDNA) memory ordering: a wave's vector stores are
+    // counted by vmcnt and the CU's L1 is write-through, so after
+    // s_waitcnt vmcnt(0) the wave's own later loads see them.  On gfx10+
+    // (stores counted by vscnt) it would need a wavefront-scope
+    // release/acquire fence instead (measured within +0.5 % here, DESIGN.md
+    // §2.1a).
     if (!camera) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t wrote = bounce_wave<STACK, MODE, true>(sc, cx, a, camera ? 0u : lvl, active, idx, slot,
                                                                  a.in_q, a.in_q, nullptr, out, 0u, lanes_below, st);

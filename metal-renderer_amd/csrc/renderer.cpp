@@ -150,6 +150,10 @@ struct Exchange {
   int pending = -1;           // buffer whose gather awaits rank 0's unpack (overlap mode)
   uint32_t next = 0;
   const mrt_comm* comm = nullptr;
+  // the communicator's shape, copied at each exchange: a deferred unpack
+  // never dereferences `comm` (it may be destroyed before the flush)
+  uint32_t rank = 0, nranks = 1;
+  uint32_t width = 0, height = 0;   // image size the pending gather was packed at
 };
 
 struct mrt_renderer {
@@ -434,13 +438,28 @@ int exchange_buffers(mrt_renderer* r, const mrt_comm* c) {
 // renderer's stream after the gather so sync/read see it complete
 int exchange_unpack(mrt_renderer* r, int i) {
   Exchange& x = r->x;
-  const mrt_comm* c = x.comm;
   HIP_TRY(hipStreamWaitEvent(r->stream, x.gather_done[i], 0));
-  if (c->rank == 0)
-    for (uint32_t k = 1; k < c->nranks; ++k)
+  if (x.rank == 0)
+    for (uint32_t k = 1; k < x.nranks; ++k)
       HIP_TRY(mrt::fast::launch_tiles_move(x.gathered.as<float4>() + (size_t)k * (x.slab_floats / 4),
-                                           reinterpret_cast<float4*>(r->image), r->desc.width, r->desc.height, k,
-                                           c->nranks, false, r->stream));
+                                           reinterpret_cast<float4*>(r->image), x.width, x.height, k,
+                                           x.nranks, false, r->stream));
+  return MRT_OK;
+}
+
+// Forget a deferred (overlapped) gather without unpacking it — its tiles
+// belong to an image that resize / reset discards.  The gather itself may
+// still be writing the receive buffer: `wait` (resize, which may reallocate
+// the exchange buffers) waits for it; reset need not (the next gather into
+// the same buffer runs after it on the communicator's stream, and nothing
+// else reads the buffer), so the overlap of the gather with the next draw
+// is kept.
+int exchange_drop(mrt_renderer* r, bool wait) {
+  Exchange& x = r->x;
+  if (x.pending < 0) return MRT_OK;
+  const int i = x.pending;
+  x.pending = -1;
+  if (wait) HIP_TRY(hipEventSynchronize(x.gather_done[i]));
   return MRT_OK;
 }
 
@@ -1089,14 +1108,19 @@ int mrt_renderer_resize(mrt_renderer* r, uint32_t width, uint32_t height) {
   if (!r->own_image) return fail(MRT_ERR_STATE, "cannot resize an externally owned image");
   int rc = finalize_pending(r);
   if (rc) return rc;
+  rc = exchange_drop(r, true);   // a pending gather was packed for the old size: never unpack it into the new image
+  if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(r->stream));
   r->desc.width = width;
   r->desc.height = height;
+  r->x.slab_floats = 0;    // the exchange buffers are re-sized for the new image at the next exchange
   return alloc_frame_buffers(r);
 }
 
 int mrt_renderer_reset(mrt_renderer* r) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  int rc = exchange_drop(r, false);   // the pre-reset frame's deferred tiles must not land in the cleared image
+  if (rc) return rc;
   // stream-ordered after the pending draws: no read-back needed here
   HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)r->desc.width * r->desc.height * 16, r->stream));
   r->frame_index = 0;
@@ -1415,6 +1439,10 @@ int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
   rc = exchange_buffers(r, c);
   if (rc) return rc;
   Exchange& x = r->x;
+  x.rank = c->rank;
+  x.nranks = c->nranks;
+  x.width = W;
+  x.height = H;
   const int i = overlap ? (int)x.next : 0;
   x.next ^= 1u;
   // the gather two exchanges ago may still be reading packed[i]

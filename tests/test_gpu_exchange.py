@@ -109,3 +109,46 @@ def test_bench_multirank_rehearsal(gpu, world):
     d = json.loads(line)
     assert d["n_gpus"] == world and d["image_check"] == "bitwise equal to the 1-GPU render"
     assert d["value"] > 0
+
+
+def test_bench_self_launches_ranks(gpu):
+    """`bench.py --gpus 2` with no launcher starts its two ranks itself (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set before any HIP call) — never a
+    silent single rank; rank 0's line reports n_gpus 2 and the bitwise image
+    check of the exchanged frame."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--exchange-backend", "host", "--check-image"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["image_check"] == "bitwise equal to the 1-GPU render"
+
+
+def test_overlapped_exchange_then_resize_reset_and_comm_close(gpu, mrt_mod):
+    """A deferred (overlapped) gather is dropped, not unpacked, by resize (the
+    buffers were packed for the old size) and by reset, and a flush after the
+    communicator was destroyed never touches it: each image equals a plain
+    render of the same frames."""
+    sc = mrt_mod.Scene("cornellbox")
+    L, frames = 3, 2
+    mode = mrt_mod.EXCHANGE_GATHER | mrt_mod.EXCHANGE_OVERLAP
+    comm = mrt_mod.Comm(mrt_mod.comm_unique_id(), 1, 0, 0)
+    r = mrt_mod.Renderer(sc, 96, 64, L)
+    r.draw(frames)
+    r.exchange(comm, mode)
+    r.resize(200, 130)                    # larger: the pending gather must not be unpacked into it
+    r.draw(frames)
+    big = r.read_image()
+    r.exchange(comm, mode)
+    r.reset()
+    r.draw(frames)
+    r.exchange(comm, mode)
+    comm.close()                          # destroyed before the deferred unpack
+    after = r.read_image()
+    r.close()
+    ref = _render(mrt_mod, sc, 200, 130, L, frames, 1)
+    assert big.tobytes() == ref.tobytes() and after.tobytes() == ref.tobytes()

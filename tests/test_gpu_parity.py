@@ -392,3 +392,47 @@ def test_debug_material_stage_and_no_accumulate_stage(gpu, mrt_mod, oracle_mod):
     oracle_mod.accumulate(7, rays, img, oracle_mod.NO_ACCUMULATE)
     mrt_mod.accumulate(sc, W, H, 7, dev_ptr(d_rays), dev_ptr(d_img), accumulate_image=False)
     assert from_dev(d_img, np.float32).tobytes() == img.tobytes()
+
+
+def test_c_cli_matches_oracle(gpu, mrt_mod, oracle_mod, tmp_path):
+    """The C host (metal-renderer_amd/cli/render.c: includes include/mrt.h,
+    links libmrt.so, built by build()) renders cornellbox 64x48, L = 4,
+    2 frames, precise, to a PFM that matches the oracle at the BASELINE.md
+    gate (the reference's app shell: macos/GameViewController.m:25-27 +
+    Renderer.h:3-8)."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(mrt_mod.LIB_PATH), "..", "bin", "mrt_render")
+    out = tmp_path / "cli.pfm"
+    p = subprocess.run([exe, "--scene", "cornellbox", "--w", "64", "--h", "48", "--spp", "2", "--L", "4",
+                        "--precise", "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    with open(out, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = map(int, f.readline().split())
+        assert float(f.readline()) < 0   # little endian
+        img = np.frombuffer(f.read(), "<f4").reshape(h, w, 3)   # bottom-up rows == ours
+    ref, A = _oscene(oracle_mod, mrt_mod, "cornellbox").render(64, 48, 4, SEED, 2, threads=8)
+    rel, rmse, same = pixel_metrics(np.concatenate([img, np.ones((h, w, 1), np.float32)], -1), ref)
+    assert (w, h) == (64, 48)
+    assert np.mean(rel <= 1e-4) >= 0.999 and rmse <= 1e-3
+    import json
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["frames"] == 2 and line["active_ray_bounces_rank0"] == A
+
+
+def test_c_cli_two_ranks_host_exchange(gpu, mrt_mod, tmp_path):
+    """mrt_render --gpus 2 --exchange host: two forked ranks (one GPU here;
+    RCCL needs one device per rank) render their tiles and rank 0 assembles
+    the frame through host memory: equal to the single-rank render bitwise."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(mrt_mod.LIB_PATH), "..", "bin", "mrt_render")
+    args = ["--scene", "cornellbox", "--w", "200", "--h", "130", "--spp", "3", "--L", "4"]
+    imgs = []
+    for extra, name in ((["--gpus", "1"], "a.pfm"), (["--gpus", "2", "--exchange", "host"], "b.pfm")):
+        p = subprocess.run([exe] + args + extra + ["--out", str(tmp_path / name)], capture_output=True, text=True,
+                           timeout=120)
+        assert p.returncode == 0, p.stderr
+        imgs.append((tmp_path / name).read_bytes())
+    assert imgs[0] == imgs[1]

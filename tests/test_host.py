@@ -293,3 +293,37 @@ def test_stream_kernel_level_bound(L):
                 assert cnt[lvl + 1] <= 127, (L, trial, cnt)
         assert runs[0] == cam
         assert all(runs[b + 1] == alive[b] for b in range(L - 1))
+
+
+def test_bench_launcher_fails_loudly_without_device():
+    """bench.py --gpus 2 without a launcher starts two ranks itself; when a rank
+    fails (here: no HIP device in this container) the job exits non-zero and
+    prints no result line — it never falls back to one rank."""
+    import json as _json
+    import subprocess
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    p = subprocess.run([_sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--config", "c1",
+                        "--steps", "1", "--warmup", "0", "--exchange-backend", "host"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert "rank" in p.stderr
+
+
+def test_bench_child_argv():
+    import importlib.util
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    saved = sys.argv
+    try:
+        sys.argv = ["bench.py", "--config", "c5", "--sweep-gpus", "1,2,4,8", "--gpus=3", "--steps", "2"]
+        argv = bench._child_argv(4)
+    finally:
+        sys.argv = saved
+    assert argv[2:] == ["--config", "c5", "--steps", "2", "--gpus", "4"]
