@@ -242,10 +242,10 @@ def cpu_baseline(cfg, frames):
         rows1 = H
         f1 = min(2, frames)
     else:
-        # one frame of a row band: a pilot band of 8 rows on all threads (it
-        # also builds the BVH) gives the rate; the band is sized to ~10 s on
-        # all threads and ~10 s on one
-        frames = 1
+        # a pilot band of 8 rows on all threads (after a first pass that
+        # builds the BVH) gives the rate: one frame of a row band sized to
+        # ~10 s on all threads, or whole frames when one takes less; ~10 s
+        # on one thread
         pilot = np.zeros((H, W), np.uint8)
         pilot[(H - 8) // 2:(H - 8) // 2 + 8] = 1
         sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, 1, threads=threads, pixel_mask=pilot, flags=B)   # BVH build
@@ -253,6 +253,8 @@ def cpu_baseline(cfg, frames):
         sc.render(W, H, cfg["L"], mrt.DEFAULT_SEED, 1, threads=threads, pixel_mask=pilot, flags=B)
         per_row = max(1e-6, (time.perf_counter() - tp) / 8)
         rows = max(1, min(H, int(10.0 / per_row)))
+        # a whole frame in < 10 s: several frames of the whole image, else one frame of the band
+        frames = max(1, min(frames, int(10.0 / (per_row * H)))) if rows == H else 1
         rows1 = max(1, min(H, int(10.0 / (per_row * threads))))
         f1 = 1
     mask = np.zeros((H, W), np.uint8)

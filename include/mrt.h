@@ -197,8 +197,10 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);
 /* drawableSizeWillChange: reallocate, frameIndex = 0 (Renderer.mm:640-657) */
 int mrt_renderer_resize(mrt_renderer* r, uint32_t width, uint32_t height);
-/* frameIndex = 0 without reallocating (the next frame overwrites the image);
- * the cumulative counters of mrt_stats are kept. */
+/* frameIndex = 0 without reallocating: the next frame overwrites every pixel
+ * the renderer owns (until then the image keeps its content; pixels written
+ * by an exchange or mrt_renderer_tiles_write, and an external image, are
+ * cleared here); the cumulative counters of mrt_stats are kept. */
 int mrt_renderer_reset(mrt_renderer* r);
 /* Generate + upload the noise tables for frames [frame_index, frame_index+n)
  * ahead of time (the reference regenerates one slot per frame on the CPU,

@@ -159,6 +159,11 @@ struct Hit {
 #ifndef MRT_ZSEL
 #define MRT_ZSEL 1
 #endif
+// MRT_PUSH3: global-memory modes push a node's other hit children with one
+// block of unconditional LDS writes instead of a branch per child
+#ifndef MRT_PUSH3
+#define MRT_PUSH3 0
+#endif
 constexpr uint32_t kQuadCopies = 4;                      // (x, y) sign quadrants
 constexpr uint32_t kQuadCopyF4 = 7;                      // six plane rows + the refs row
 constexpr uint32_t kQuadNodeF4 = kQuadCopies * kQuadCopyF4;
@@ -479,9 +484,39 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     }
     MRT_CE(0, 1) MRT_CE(2, 3) MRT_CE(0, 2) MRT_CE(1, 3) MRT_CE(1, 2)
 #undef MRT_CE
-    if (t[3] < inf) { stack_push<STACK>(cx, sp, r[3]); ++sp; }
-    if (t[2] < inf) { stack_push<STACK>(cx, sp, r[2]); ++sp; }
-    if (t[1] < inf) { stack_push<STACK>(cx, sp, r[1]); ++sp; }
+#if MRT_PUSH3
+    if (MODE != kAllLds) {
+      // the hit children after the nearest, far to near, as one block of
+      // three unconditional LDS writes (slots above the new top take
+      // garbage) when the three slots are LDS-resident: no per-child branch
+      const int c = (int)(t[1] < inf) + (int)(t[2] < inf) + (int)(t[3] < inf);
+      const int32_t v0 = c == 3 ? r[3] : (c == 2 ? r[2] : r[1]);
+      const int32_t v1 = c == 3 ? r[2] : r[1];
+      constexpr int kL = STACK < 0 ? -STACK : STACK;
+      if (STACK > 0 || sp + 3 <= kL) {
+        uint32_t* st = lds_u32() + cx.stack_base + threadIdx.x + sp * kBlock;
+        if (STACK > 0 && sp + 3 > kL) {   // full-LDS stacks never overflow: write only the live entries
+          if (c > 0) st[0] = (uint32_t)v0;
+          if (c > 1) st[kBlock] = (uint32_t)v1;
+          if (c > 2) st[2 * kBlock] = (uint32_t)r[1];
+        } else {
+          st[0] = (uint32_t)v0;
+          st[kBlock] = (uint32_t)v1;
+          st[2 * kBlock] = (uint32_t)r[1];
+        }
+      } else {
+        if (c > 0) stack_push<STACK>(cx, sp, v0);
+        if (c > 1) stack_push<STACK>(cx, sp + 1, v1);
+        if (c > 2) stack_push<STACK>(cx, sp + 2, r[1]);
+      }
+      sp += c;
+    } else
+#endif
+    {
+      if (t[3] < inf) { stack_push<STACK>(cx, sp, r[3]); ++sp; }
+      if (t[2] < inf) { stack_push<STACK>(cx, sp, r[2]); ++sp; }
+      if (t[1] < inf) { stack_push<STACK>(cx, sp, r[1]); ++sp; }
+    }
     int32_t next = r[0];
     if (!(t[0] < inf)) next = stack_pop<STACK>(cx, sp);
     return next;
@@ -1446,10 +1481,12 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
 // batch instead of one per bounce.  The arithmetic of every path is the
 // same, so the image is identical (precise build: bitwise).
 // LDS path state per lane ([word][lane] after the stack): T (0-2), R (3-5),
-// material pdf (6), ior (7), next-ray origin (8-10) and direction (11-13),
-// pixel slot tag (14), flags (15: prevDiffuse).
+// material pdf (6), ior (7), next-ray direction (8-10), pixel slot tag |
+// prevDiffuse << 31 (11).  The next ray's origin needs no word: it is the
+// shadow ray's origin (both are p + n * 1e-4, Shaders.metal:171,205), which
+// stays in the lane's ray registers through the shadow query.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPathStateWords = 16;
+constexpr uint32_t kPathStateWords = 12;
 #ifndef MRT_PATH_WAVES   // 5: 96 VGPRs with 1-3 spilled values (C4 +11 %, C3 +8 % over 4 waves)
 #define MRT_PATH_WAVES 5
 #endif
@@ -1523,8 +1560,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
           ps[0 * kBlock] = fbits(1.0f); ps[1 * kBlock] = fbits(1.0f); ps[2 * kBlock] = fbits(1.0f);
           ps[3 * kBlock] = 0u; ps[4 * kBlock] = 0u; ps[5 * kBlock] = 0u;
           ps[6 * kBlock] = fbits(1.0f); ps[7 * kBlock] = fbits(1.00029f);
-          ps[14 * kBlock] = idx;
-          ps[15 * kBlock] = 0u;
+          ps[11 * kBlock] = idx;   // prevDiffuse 0
           phase = 1;
           bounce = 0;
           trav_begin(sc, tr);
@@ -1569,8 +1605,9 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       s.R = mk(bitsf(ps[3 * kBlock]), bitsf(ps[4 * kBlock]), bitsf(ps[5 * kBlock]));
       s.pdf = bitsf(ps[6 * kBlock]);
       s.ior = bitsf(ps[7 * kBlock]);
-      s.prevDiffuse = (ps[15 * kBlock] & 1u) ? 1.0f : 0.0f;
-      const uint32_t gslot = ps[14 * kBlock];
+      const uint32_t tagv = ps[11 * kBlock];
+      s.prevDiffuse = (tagv >> 31) ? 1.0f : 0.0f;
+      const uint32_t gslot = tagv & 0x7FFFFFFFu;
       const bool last = bounce + 1 == L;
       const bool hit_ok = h.found && !(h.t < kDistanceEpsilon);   // :122-126
       ShadowRay sh;
@@ -1590,21 +1627,20 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         ps[0 * kBlock] = fbits(s.T.x); ps[1 * kBlock] = fbits(s.T.y); ps[2 * kBlock] = fbits(s.T.z);
         ps[3 * kBlock] = fbits(s.R.x); ps[4 * kBlock] = fbits(s.R.y); ps[5 * kBlock] = fbits(s.R.z);
         ps[6 * kBlock] = fbits(s.pdf); ps[7 * kBlock] = fbits(s.ior);
-        ps[8 * kBlock] = fbits(s.o.x); ps[9 * kBlock] = fbits(s.o.y); ps[10 * kBlock] = fbits(s.o.z);
-        ps[11 * kBlock] = fbits(s.d.x); ps[12 * kBlock] = fbits(s.d.y); ps[13 * kBlock] = fbits(s.d.z);
-        ps[15 * kBlock] = s.prevDiffuse != 0.0f ? 1u : 0u;
+        ps[8 * kBlock] = fbits(s.d.x); ps[9 * kBlock] = fbits(s.d.y); ps[10 * kBlock] = fbits(s.d.z);
+        ps[11 * kBlock] = gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u);
+        ro = s.o;   // the next ray's origin (also the shadow ray's, below)
         // the shadow ray: MPS nearest hit == target test + occlusion query
         bool shadow = false;
         if (sh.valid) {
           const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
           const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
           float tT, u, v;
-          if (tri_test(sh.o, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
+          if (tri_test(ro, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
               !(tT < kDistanceEpsilon)) {
             shadow = true;
             phase = 2;
-            ro = sh.o;
-            rd = sh.d;
+            rd = sh.d;   // ro = s.o = sh.o
             trav_begin(sc, tr);
             h.t = tT;
             h.u = sh.L.x;
@@ -1622,8 +1658,8 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
     if (next_query) {
       bounce += 1;
       atomicAdd(&s_count[bounce - 1], 1u);   // stats: rays alive at the start of this bounce
-      ro = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
-      rd = mk(bitsf(ps[11 * kBlock]), bitsf(ps[12 * kBlock]), bitsf(ps[13 * kBlock]));
+      // ro already holds the next ray's origin (set at shading, unchanged by a shadow query)
+      rd = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
       phase = 1;
       trav_begin(sc, tr);
       h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;

@@ -104,7 +104,8 @@ struct mrt_scene {
 
 // bookkeeping of one draw_n call whose statistics are not read back yet
 struct DrawRecord {
-  DevBuf counters;                          // per (batch, bounce) survivor totals
+  DevBuf counters;                          // per (batch, bounce) survivor totals, then the launches' grab
+                                            // counters (one buffer: one memset per draw)
   hipEvent_t start = nullptr, stop = nullptr;
   std::vector<hipEvent_t> kernel_events;    // MRT_FLAG_PROFILE: 2 per timed bounce launch
   uint32_t frames = 0;
@@ -169,7 +170,7 @@ struct mrt_renderer {
   uint32_t max_frames = 0;   // MAX_FRAMES (0 = unlimited)
   uint32_t inflight = 1;   // frames in flight (MRT_INFLIGHT): with dynamic work distribution and
                            // 8-frame batches one stream is as fast as 3 (C2) and launches do not overlap
-  DevBuf grabs;             // per (launch) grab counters of the dynamic work distribution
+  bool image_foreign = false;   // the image holds pixels this renderer did not render (exchange / tiles_write)
   uint32_t grid = 0;        // persistent grid of the bounce kernel
   // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
   DevBuf noise_init, noise_window;
@@ -312,6 +313,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
     HIP_TRY(hipMalloc(&r->image, (size_t)W * H * 16));
   }
   HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)W * H * 16, r->stream));
+  r->image_foreign = false;
   r->frame_index = 0;
   r->stats = mrt_stats{};
   r->stats.owned_pixels = r->owned_pixels;
@@ -1121,8 +1123,14 @@ int mrt_renderer_reset(mrt_renderer* r) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");
   int rc = exchange_drop(r, false);   // the pre-reset frame's deferred tiles must not land in the cleared image
   if (rc) return rc;
-  // stream-ordered after the pending draws: no read-back needed here
-  HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)r->desc.width * r->desc.height * 16, r->stream));
+  // The next frame (f = 0) overwrites every pixel this renderer owns, and
+  // pixels it does not own stay 0 — unless an exchange wrote other ranks'
+  // tiles into the image: only then is it cleared (stream-ordered after
+  // the pending draws).  An external image is always cleared.
+  if (r->image_foreign || !r->own_image) {
+    HIP_TRY(hipMemsetAsync(r->image, 0, (size_t)r->desc.width * r->desc.height * 16, r->stream));
+    r->image_foreign = false;
+  }
   r->frame_index = 0;
   r->stats.frame_index = 0;   // cumulative counters (paths, A, kernel time) persist
   return MRT_OK;
@@ -1146,12 +1154,13 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   const uint32_t L = r->desc.max_path_length;
   const uint32_t B = r->batch;
   const uint32_t nb = (n + B - 1) / B;   // launches of up to B frames each
-  const size_t counter_bytes = (size_t)nb * L * 4;
+  // survivor counters [nb * L] and, 128-B aligned after them, the grab
+  // counters of every launch of the draw: zeroed by ONE memset
+  const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
+  const size_t grab_off = ((size_t)nb * L + 31) / 32 * 32;   // words
+  const size_t counter_bytes = (grab_off + (size_t)nb * L * grab_words) * 4;
   if (d.counters.bytes < counter_bytes) HIP_TRY(d.counters.alloc(counter_bytes));
   HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, r->stream));
-  const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
-  if (r->grabs.bytes < (size_t)nb * L * grab_words * 4) HIP_TRY(r->grabs.alloc((size_t)nb * L * grab_words * 4));
-  HIP_TRY(hipMemsetAsync(r->grabs.p, 0, (size_t)nb * L * grab_words * 4, r->stream));
   const uint32_t launches_per_batch = r->path_mode || r->stream_mode ? 1u : L;
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
@@ -1193,7 +1202,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.out_seg_count = seg + (size_t)(b & 1) * 2 * r->grid;
       a.out_chunk = meta + (b & 1);
       a.out_total = cnt + (size_t)k * L + b;
-      a.grab = r->grabs.as<uint32_t>() + ((size_t)k * L + b) * grab_words;
+      a.grab = d.counters.as<uint32_t>() + grab_off + ((size_t)k * L + b) * grab_words;
       for (int p = 0; p < 4; ++p) {
         a.in_q.plane[p] = fs.queue[b & 1][p].as<float4>();
         a.out_q.plane[p] = fs.queue[(b + 1) & 1][p].as<float4>();
@@ -1432,6 +1441,7 @@ int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
   int rc = exchange_flush(r);   // the previous overlapped gather's unpack (rank 0)
   if (rc) return rc;
   const uint32_t W = r->desc.width, H = r->desc.height;
+  if (c->rank == 0 && c->nranks > 1) r->image_foreign = true;   // other ranks' tiles land in rank 0's image
   if (kind == MRT_EXCHANGE_REDUCE) {   // one in-place SUM reduce of the RGBA32F image to rank 0
     NCCL_TRY(ncclReduce(r->image, r->image, (size_t)W * H * 4, ncclFloat, ncclSum, 0, c->comm, r->stream));
     return MRT_OK;
@@ -1498,6 +1508,7 @@ int mrt_renderer_tiles_write(mrt_renderer* r, uint32_t shard_rank, const float* 
   if (floats < n) return fail(MRT_ERR_INVALID, "mrt_renderer_tiles_write: buffer too small");
   rc = exchange_flush(r);
   if (rc) return rc;
+  r->image_foreign = true;
   HIP_TRY(hipStreamSynchronize(r->stream));   // the staging buffer may still feed a queued copy
   if (r->x.staging.bytes < n * 4) HIP_TRY(r->x.staging.alloc(n * 4));
   HIP_TRY(hipMemcpyAsync(r->x.staging.p, host, n * 4, hipMemcpyHostToDevice, r->stream));
