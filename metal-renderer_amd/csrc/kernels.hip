@@ -1621,7 +1621,11 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         shade_hit<MODE>(sc, cx, h, s, ns, bounce, L, !last, sh, (a.flags & kShadeDebugMaterial) != 0);
       }
       if (!hit_ok || last) {   // the path ends: accumulateImage input (Shaders.metal:233-249)
-        a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
+        // streamed once to the accumulate pass: a non-temporal store, so the
+        // 2 GB of radiance per launch do not evict BVH lines from L2 (C4
+        // +1.2 %, 1960 -> 1984 Mpaths/s, A/B twice in one call)
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(v4f{s.R.x, s.R.y, s.R.z, 0.0f}, reinterpret_cast<v4f*>(a.radiance + gslot));
         phase = 0;
       } else {
         ps[0 * kBlock] = fbits(s.T.x); ps[1 * kBlock] = fbits(s.T.y); ps[2 * kBlock] = fbits(s.T.z);
@@ -1631,8 +1635,9 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         ps[11 * kBlock] = gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u);
         ro = s.o;   // the next ray's origin (also the shadow ray's, below)
         // the shadow ray: MPS nearest hit == target test + occlusion query
+        // (MRT_DEBUG bit 1, ablation only: no shadow queries)
         bool shadow = false;
-        if (sh.valid) {
+        if (sh.valid && !(a.debug & 1u)) {
           const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
           const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
           float tT, u, v;
