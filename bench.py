@@ -230,7 +230,7 @@ def cpu_baseline(cfg, frames):
     threads = host_threads()
     if cfg["procedural"]:
         # the product's flattened scene (the seeded procedural mesh is built by
-        # libmrt's scene import; the oracle brute-forces the same buffers)
+        # libmrt's scene import; the oracle builds its BVH over the same buffers)
         e = mrt.Scene(cfg["scene"], resolve_mtl(cfg), procedural_triangles=cfg["procedural"], device=-1).export()
         sc = oracle.OracleScene.from_arrays(e["vertices"], e["references"], e["materials"])
     else:
@@ -350,6 +350,7 @@ def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_
     out.update({k: roofs[bound][k] for k in ("achieved", "peak", "unit", "frac", "frac_vs_step")})
     out.update({"bound": bound, "traffic": traffic, "roofs": roofs,
                 "wait_any_frac": pmc.get("wait_any_frac"),
+                "valu_lane_util": pmc.get("valu_lane_util"),
                 "pmc_clock_ghz": pmc.get("clock_ghz"),
                 "rocprof_avg_launch_ms": round(pmc["avg_launch_ns_rocprof"] / 1e6, 4)
                 if pmc.get("avg_launch_ns_rocprof") else None,
@@ -472,15 +473,24 @@ def main():
 
     # Roofline of the dominant kernel (stream_kernel on C1/C2, path_kernel on
     # C3-C5: one launch per frame batch), its launch time measured live with
-    # HIP events on the renderer's stream around every 8th batch's launch
-    # (timing events serialise a stream, so not every launch is timed).
+    # HIP events on the render stream around each batch's launch.  A tile
+    # share renders batches on two streams (the next launch starts while one
+    # drains), where events would also time the wait for CUs: there the
+    # launch time is the device-measured span (earliest block start to latest
+    # wave end, the chip's wall clock), which libmrt records for every batch.
     A = st["active_ray_bounces"] - base["active_ray_bounces"]
     P = st["paths"] - base["paths"]
     launches = st["kernel_launches"] - base["kernel_launches"]
     timed = st["timed_launches"] - base["timed_launches"]
     kms = st["kernel_ms"] - base["kernel_ms"]
+    spans = st["spans"] - base["spans"]
+    avg_span_ms = (st["span_ms"] - base["span_ms"]) / spans if spans else None
     bytes_alg = B_PATH * P + B_BOUNCE * A
     avg_launch_ms = kms / max(1, timed)
+    launch_timing = "hip-events on the render stream"
+    if st["inflight"] > 1 and spans and spans == launches:
+        avg_launch_ms, timed = avg_span_ms, spans
+        launch_timing = "device spans (launches on 2 streams overlap)"
     launch_s = avg_launch_ms * 1e-3
     launches_per_step = launches / max(1, args.steps)
     roof = roofline(args, pmc_path=args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json"),
@@ -500,6 +510,8 @@ def main():
                    2: "stream_kernel (wave-local streaming wavefront: all bounces per launch)"}.get(
                        st["kernel"], "bounce_kernel (one launch per bounce)"),
         "launches": launches, "timed_launches": timed, "avg_launch_ms": round(avg_launch_ms, 4),
+        "launch_timing": launch_timing,
+        "avg_span_ms": None if avg_span_ms is None else round(avg_span_ms, 4),
         "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
         "active_ray_bounces_per_step": int(A / max(1, args.steps))})
 

@@ -192,6 +192,10 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
   uint64_t timed_launches;         /* launches behind kernel_ms (every 8th frame's) */
   uint32_t kernel;                 /* the hot kernel: 0 = wavefront of per-bounce launches, 1 = path megakernel,
                                       2 = streaming wavefront (all bounces of a frame batch in one launch) */
+  uint32_t inflight;               /* frame batches in flight (render streams); > 1: launches overlap */
+  double span_ms;                  /* summed device-measured spans of the frame batches' render launches
+                                      (earliest block start to latest wave end, chip wall clock) */
+  uint64_t spans;                  /* frame batches behind span_ms (every batch) */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);

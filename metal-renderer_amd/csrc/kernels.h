@@ -94,6 +94,8 @@ struct BounceArgs {
   uint32_t* stack_spill;       // traversal stack entries beyond the LDS capacity:
                                // [grid * 256][max_stack] uint32 (null if none)
   uint32_t* bounce_counts;     // path / stream kernel: [max_path_length] rays alive at the start of bounce b + 1
+  unsigned long long* span;    // [2] of the frame batch, zeroed: ~(earliest block start), latest wave end
+                               // (wall_clock64 ticks; null = not recorded)
 };
 
 // running-mean accumulation of one frame over the owned tiles

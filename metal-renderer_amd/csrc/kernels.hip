@@ -446,6 +446,23 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
 // Both results are independent of the visiting order, so every tree (host
 // SAH, device LBVH / PLOC) returns the same (brute-force) answer.
 constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
+// Traversal slack: the interior loop of a while-while round ends once at
+// most this many lanes still seek a leaf, instead of waiting for the last
+// one (the lanes holding a leaf test it; the others resume next round).  The
+// path kernel's rounds are resumable anyway, and in deep global-memory trees
+// the last lanes' descents are long: slack 12 (of 64) measured C4 1950 ->
+// 2497 Mpaths/s (+28 %), C3 +7.5 %, C3g +5 %, C5 1/8 share +28 % (8 / 16 /
+// 24 / 32 / 48: C4 2456 / 2488 / 2397 / 2281 / 1904).  Shallow all-in-LDS
+// trees lose by it (C2, the stream kernel: slack 2 -1.3 %, 8 -3.4 %).
+#ifndef MRT_TRAV_SLACK   // traverse(): stream / bounce / stage kernels
+#define MRT_TRAV_SLACK 0
+#endif
+#ifndef MRT_PATH_SLACK   // trav_round(): the path kernel
+#define MRT_PATH_SLACK 12
+#endif
+#ifndef MRT_LEAF_SLACK   // trav_round(): the leaf loop's (a kept leaf is tested next round)
+#define MRT_LEAF_SLACK 0
+#endif
 
 template <int STACK>
 __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
@@ -581,7 +598,7 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
         leaf = node;
         node = stack_pop<STACK>(cx, sp);
       }
-      if (!__any(leaf == 0)) break;
+      if ((uint32_t)__popcll(__ballot(leaf == 0)) <= (uint32_t)MRT_TRAV_SLACK) break;
     }
     // leaves
     while (leaf < 0) {
@@ -1184,11 +1201,23 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   return wrote;
 }
 
+// Device-measured execution span of a frame batch's render launch(es): the
+// earliest block start and the latest wave end on the chip's wall clock.
+// With batches on two streams the next launch's blocks start while this one
+// drains, so host events around a launch would time the wait as well.
+__device__ __forceinline__ void span_begin(const BounceArgs& a) {
+  if (a.span && threadIdx.x == 0) atomicMax(a.span, ~(unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void span_end(const BounceArgs& a) {
+  if (a.span && (threadIdx.x & 63u) == 0) atomicMax(a.span + 1, (unsigned long long)wall_clock64());
+}
+
 template <int STACK, int MODE>
 __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_wave[kBlock / 64];
   __shared__ uint32_t s_cursor[2], s_res, s_closed;
   STAMP_ENTRY();
+  span_begin(a);
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
@@ -1303,6 +1332,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     if (total) atomicAdd(a.out_total, total);   // stats: one atomic per block per launch
     if (blockIdx.x == 0) *a.out_chunk = cap;
   }
+  span_end(a);
 }
 
 
@@ -1331,6 +1361,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
   __shared__ uint32_t s_cnt[kBlock / 64][kStreamMaxL];    // rays queued per level (wave-private rows)
   __shared__ uint32_t s_alive[kBlock / 64][kStreamMaxL];  // survivors per bounce (stats)
   __shared__ uint32_t s_closed;
+  span_begin(a);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t L = a.max_path_length;
   const LdsCtx cx = stage_lds<MODE>(sc, 0, a.stack_spill);
@@ -1417,6 +1448,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
   // stats: survivors of bounce b = rays alive at the start of bounce b + 1
   for (uint32_t b = lane; b + 1 < L; b += 64u)
     if (s_alive[wave][b]) atomicAdd(a.bounce_counts + b, s_alive[wave][b]);
+  span_end(a);
 }
 
 struct Trav {
@@ -1447,7 +1479,7 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
       tr.leaf = tr.node;
       tr.node = stack_pop<STACK>(cx, tr.sp);
     }
-    if (!__any(tr.leaf == 0)) break;
+    if ((uint32_t)__popcll(__ballot(tr.leaf == 0)) <= (uint32_t)MRT_PATH_SLACK) break;
   }
   while (tr.leaf < 0) {
     const uint32_t lr = ~(uint32_t)tr.leaf;
@@ -1463,6 +1495,9 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
       tr.leaf = tr.node;
       tr.node = stack_pop<STACK>(cx, tr.sp);
     }
+#if MRT_LEAF_SLACK > 0
+    if ((uint32_t)__popcll(__ballot(tr.leaf < 0)) <= (uint32_t)MRT_LEAF_SLACK) break;
+#endif
   }
 }
 
@@ -1498,6 +1533,7 @@ template <int STACK, int MODE>
 __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_closed;
   __shared__ uint32_t s_count[64];   // rays alive at the start of bounce b + 1 (stats)
+  span_begin(a);
   const uint32_t tid = threadIdx.x;
   const LdsCtx cx = stage_lds<MODE>(sc, 1, a.stack_spill);
   if (tid == 0) s_closed = 0;
@@ -1672,6 +1708,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   }
   __syncthreads();
   if (tid < 64 && tid + 1 < L && s_count[tid]) atomicAdd(a.bounce_counts + tid, s_count[tid]);
+  span_end(a);
 }
 
 // accumulateImage (renderer/Shaders.metal:233-249) for a batch of frames over

@@ -107,19 +107,22 @@ struct DrawRecord {
   DevBuf counters;                          // per (batch, bounce) survivor totals, then the launches' grab
                                             // counters (one buffer: one memset per draw)
   hipEvent_t start = nullptr, stop = nullptr;
+  hipEvent_t cleared = nullptr;             // the counters' memset (other render streams of the draw wait on it)
   std::vector<hipEvent_t> kernel_events;    // MRT_FLAG_PROFILE: 2 per timed bounce launch
   uint32_t frames = 0;
   uint32_t launches = 0;                    // batches (bounce launches = batches * L)
+  size_t span_off = 0;                      // byte offset of the batches' [2] u64 spans in `counters`
+  size_t counter_bytes = 0;                 // bytes of `counters` this draw uses
   size_t events = 0;
   bool pending = false;
 };
 constexpr int kDrawRing = 3;
 
 // One in-flight frame: its queues, segment counts, per-pixel path radiance and
-// the stream its bounce launches run on.  Frames f and f+1 run on different
+// the stream its render launches run on.  Batches b and b+1 run on different
 // slots concurrently (the reference keeps up to 3 frames in flight,
-// renderer/Renderer.mm:16,593-600); their accumulations are chained in frame
-// order with events because the running mean is order-dependent.
+// renderer/Renderer.mm:16,593-600); their accumulations run in order on the
+// main stream because the running mean is order-dependent.
 struct FrameSlot {
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -127,7 +130,9 @@ struct FrameSlot {
   DevBuf segments;          // 2 queues x 2 classes x grid per-block survivor counts + 2 chunk words
   DevBuf radiance;          // W*H float4, written once per owned pixel per frame
   DevBuf spill;             // traversal stack entries beyond the LDS capacity (deep BVHs)
-  hipEvent_t acc_done = nullptr;
+  hipEvent_t acc_done = nullptr;      // on the main stream: the accumulate that last read `radiance`
+  hipEvent_t kernel_done = nullptr;   // on `stream`: its last render launch
+  bool acc_recorded = false;
 };
 
 // RCCL communicator of one rank (one process per GPU) and the stream its
@@ -168,8 +173,17 @@ struct mrt_renderer {
   uint64_t owned_pixels = 0;
   std::vector<FrameSlot> slots;
   uint32_t max_frames = 0;   // MAX_FRAMES (0 = unlimited)
-  uint32_t inflight = 1;   // frames in flight (MRT_INFLIGHT): with dynamic work distribution and
-                           // 8-frame batches one stream is as fast as 3 (C2) and launches do not overlap
+  // Frame batches in flight (MRT_INFLIGHT; default 1 for a whole frame, 2 for a
+  // tile share).  With k >= 2 every slot renders on its own stream and the
+  // accumulates run on the main stream, so batch b + 1 (of this draw or the
+  // next) only waits for the accumulate that last read its slot's radiance:
+  // its persistent blocks take the CUs as batch b's drain (~0.2 ms per
+  // launch, whatever its length) frees them.  One GPU's 1/8 tile share of C2
+  // launches 2.1-ms kernels, where that drain is 10 %.
+  uint32_t inflight = 1;
+  uint32_t slot_next = 0;   // slot of the next batch (rotates across draws)
+  hipStream_t readback = nullptr;   // draw statistics read-back (never waits for queued work)
+  double wall_khz = 0.0;    // device wall clock (span timestamps; 0 = spans off, MRT_SPANS=0)
   bool image_foreign = false;   // the image holds pixels this renderer did not render (exchange / tiles_write)
   uint32_t grid = 0;        // persistent grid of the bounce kernel
   // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
@@ -202,8 +216,13 @@ int finalize_draw(mrt_renderer* r, DrawRecord& d) {
   float ms = 0.0f;
   HIP_TRY(hipEventElapsedTime(&ms, d.start, d.stop));
   const uint32_t L = r->desc.max_path_length;
-  std::vector<uint32_t> cnt((size_t)d.launches * L);
-  HIP_TRY(hipMemcpy(cnt.data(), d.counters.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+  // one copy of the whole counter buffer (survivor counts, grab counters,
+  // spans) on the renderer's private read-back stream: the draw is complete
+  // (its stop event has fired), and nothing queued after it is waited for
+  std::vector<uint32_t> buf((d.counter_bytes + 3) / 4);
+  HIP_TRY(hipMemcpyAsync(buf.data(), d.counters.p, d.counter_bytes, hipMemcpyDeviceToHost, r->readback));
+  HIP_TRY(hipStreamSynchronize(r->readback));
+  const uint32_t* cnt = buf.data();
   uint64_t active = r->owned_pixels * d.frames;   // bounce 0: every owned pixel's camera ray
   for (uint32_t k = 0; k < d.launches; ++k)
     for (uint32_t b = 0; b + 1 < L; ++b) active += cnt[(size_t)k * L + b];
@@ -212,6 +231,17 @@ int finalize_draw(mrt_renderer* r, DrawRecord& d) {
   const uint64_t paths = r->owned_pixels * d.frames;
   r->stats.mpaths_per_s = ms > 0.0f ? (double)paths / (ms * 1e-3) / 1e6 : 0.0;
   r->stats.kernel_launches += (uint64_t)d.launches * (r->path_mode || r->stream_mode ? 1u : L);
+  {
+    std::vector<unsigned long long> sp((size_t)2 * d.launches);
+    std::memcpy(sp.data(), reinterpret_cast<const char*>(buf.data()) + d.span_off, sp.size() * 8);
+    for (uint32_t k = 0; k < d.launches; ++k) {
+      const unsigned long long t0 = ~sp[2 * k], t1 = sp[2 * k + 1];
+      if (sp[2 * k] && t1 >= t0 && r->wall_khz > 0.0) {
+        r->stats.span_ms += (double)(t1 - t0) / r->wall_khz;
+        r->stats.spans += 1;
+      }
+    }
+  }
   if (r->desc.flags & MRT_FLAG_PROFILE) {
     for (size_t k = 0; k + 1 < d.events; k += 2) {
       float ms_k = 0.0f;
@@ -318,6 +348,10 @@ int alloc_frame_buffers(mrt_renderer* r) {
   r->stats = mrt_stats{};
   r->stats.owned_pixels = r->owned_pixels;
   r->stats.kernel = r->path_mode ? 1u : (r->stream_mode ? 2u : 0u);
+  r->stats.inflight = r->inflight;
+  // the render streams do not wait on the main stream: its memsets above
+  // (segments, image) complete before any batch is queued
+  HIP_TRY(hipStreamSynchronize(r->stream));
   return MRT_OK;
 }
 
@@ -1047,6 +1081,7 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   for (DrawRecord& d : r->draws) {
     HIP_TRY(hipEventCreate(&d.start));
     HIP_TRY(hipEventCreate(&d.stop));
+    HIP_TRY(hipEventCreateWithFlags(&d.cleared, hipEventDisableTiming));
   }
   // LDS stack capacity: the BVH's bound rounded up to 8/16 entries when it is
   // <= 16; deeper BVHs keep 8 entries in LDS and spill the rest to global
@@ -1063,18 +1098,28 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
   if (const char* v = std::getenv("MRT_PROFILE_EVERY"))
     r->profile_every = std::max<uint32_t>(1, (uint32_t)std::strtoul(v, nullptr, 0));
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, desc->scene->device) == hipSuccess)
+      r->wall_khz = (double)khz;
+  }
+  HIP_TRY(hipStreamCreateWithFlags(&r->readback, hipStreamNonBlocking));
+  if (const char* v = std::getenv("MRT_SPANS"))
+    if (std::atoi(v) == 0) r->wall_khz = 0.0;
+  r->inflight = S > 1 ? 2u : 1u;
   if (const char* v = std::getenv("MRT_INFLIGHT")) r->inflight = (uint32_t)std::strtoul(v, nullptr, 0);
   r->inflight = std::max<uint32_t>(1, std::min<uint32_t>(8, r->inflight));
   r->slots.resize(r->inflight);
   for (uint32_t k = 0; k < r->inflight; ++k) {
     FrameSlot& fs = r->slots[k];
-    if (k == 0) {
+    if (r->inflight == 1) {   // one slot: everything in order on the main stream
       fs.stream = r->stream;
     } else {
       HIP_TRY(hipStreamCreateWithFlags(&fs.stream, hipStreamNonBlocking));
       fs.own_stream = true;
     }
     HIP_TRY(hipEventCreateWithFlags(&fs.acc_done, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&fs.kernel_done, hipEventDisableTiming));
   }
   // kernel: scenes traversed from global memory run the path megakernel (all
   // bounces of a frame batch in one launch: C3 +15 %, C4 +1.5 % over the
@@ -1087,8 +1132,8 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::path_grid(r->scene->dev, r->stack_entries, &r->grid)
                                              : mrt::fast::path_grid(r->scene->dev, r->stack_entries, &r->grid));
   else
-    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid)
-                                             : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, r->inflight > 1 ? 3u : 0u, &r->grid));
+    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid)
+                                             : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid));
   if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
   // streaming wavefront (one launch per frame batch, per-wave ray queues)
   // for whole-scene-in-LDS scenes; MRT_STREAM=0 keeps one launch per bounce
@@ -1158,9 +1203,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   // counters of every launch of the draw: zeroed by ONE memset
   const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
   const size_t grab_off = ((size_t)nb * L + 31) / 32 * 32;   // words
-  const size_t counter_bytes = (grab_off + (size_t)nb * L * grab_words) * 4;
+  const size_t span_off = (grab_off + (size_t)nb * L * grab_words + 1) / 2 * 8;   // bytes, 8-B aligned
+  const size_t counter_bytes = span_off + (size_t)nb * 16;
   if (d.counters.bytes < counter_bytes) HIP_TRY(d.counters.alloc(counter_bytes));
-  HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, r->stream));
   const uint32_t launches_per_batch = r->path_mode || r->stream_mode ? 1u : L;
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
@@ -1172,14 +1217,26 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     }
   }
   HIP_TRY(hipEventRecord(d.start, r->stream));
-  for (uint32_t k = 1; k < r->inflight; ++k) HIP_TRY(hipStreamWaitEvent(r->slots[k].stream, d.start, 0));
+  // The render launches never wait on the main stream (it only carries
+  // accumulates and image work; the noise window is uploaded synchronously):
+  // the counters are cleared on the first batch's render stream and the
+  // draw's other render streams wait for that.
+  const uint32_t s0 = r->slot_next;
+  HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, r->slots[s0].stream));
+  if (r->inflight > 1 && nb > 1) {
+    HIP_TRY(hipEventRecord(d.cleared, r->slots[s0].stream));
+    for (uint32_t j = 1; j < std::min(nb, r->inflight); ++j)
+      HIP_TRY(hipStreamWaitEvent(r->slots[(s0 + j) % r->inflight].stream, d.cleared, 0));
+  }
   uint32_t* cnt = d.counters.as<uint32_t>();
   size_t ev = 0;
-  const FrameSlot* prev = nullptr;
   for (uint32_t k = 0; k < nb; ++k) {
     const uint64_t f = r->frame_index + (uint64_t)k * B;
     const uint32_t batch = std::min<uint32_t>(B, n - k * B);
-    FrameSlot& fs = r->slots[k % r->inflight];
+    FrameSlot& fs = r->slots[(s0 + k) % r->inflight];
+    const bool own = fs.stream != r->stream;
+    // the slot's radiance is free once the accumulate that last read it ran
+    if (own && fs.acc_recorded) HIP_TRY(hipStreamWaitEvent(fs.stream, fs.acc_done, 0));
     uint32_t* seg = fs.segments.as<uint32_t>();
     uint32_t* meta = seg + 4 * (size_t)r->grid;
     for (uint32_t b = 0; b < launches_per_batch; ++b) {
@@ -1212,6 +1269,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.radiance = fs.radiance.as<float4>();
       a.stack_spill = fs.spill.as<uint32_t>();
       a.bounce_counts = cnt + (size_t)k * L;
+      a.span = r->wall_khz > 0.0
+                   ? reinterpret_cast<unsigned long long*>(static_cast<char*>(d.counters.p) + span_off) + 2 * k
+                   : nullptr;
       const bool timed = profile && (k % r->profile_every) == 0;
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
       if (r->path_mode) HIP_TRY(launch_paths(r, a, fs.stream));
@@ -1219,9 +1279,12 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       else HIP_TRY(launch_bounce(r, a, fs.stream));
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
     }
-    // accumulateImage for frames f .. f+batch-1, after the previous batch's
-    // (running mean order)
-    if (prev && prev != &fs) HIP_TRY(hipStreamWaitEvent(fs.stream, prev->acc_done, 0));
+    // accumulateImage for frames f .. f+batch-1 on the main stream, in batch
+    // order (the running mean's order), behind this batch's render launch
+    if (own) {
+      HIP_TRY(hipEventRecord(fs.kernel_done, fs.stream));
+      HIP_TRY(hipStreamWaitEvent(r->stream, fs.kernel_done, 0));
+    }
     mrt::AccumArgs acc{};
     acc.width = r->desc.width;
     acc.height = r->desc.height;
@@ -1234,16 +1297,17 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     acc.radiance = fs.radiance.as<float4>();
     acc.image = reinterpret_cast<float4*>(r->image);
     acc.accumulate = (r->desc.flags & MRT_FLAG_NO_ACCUMULATE) ? 0u : 1u;
-    HIP_TRY(launch_accumulate_frame(r, acc, fs.stream));
-    HIP_TRY(hipEventRecord(fs.acc_done, fs.stream));
-    prev = &fs;
+    HIP_TRY(launch_accumulate_frame(r, acc, r->stream));
+    HIP_TRY(hipEventRecord(fs.acc_done, r->stream));
+    fs.acc_recorded = true;
   }
-  // join every slot back into the main stream
-  for (uint32_t k = 1; k < r->inflight && k < nb; ++k) HIP_TRY(hipStreamWaitEvent(r->stream, r->slots[k].acc_done, 0));
+  r->slot_next = (s0 + nb) % r->inflight;
   HIP_TRY(hipEventRecord(d.stop, r->stream));
   d.pending = true;
   d.frames = n;
   d.launches = nb;
+  d.span_off = span_off;
+  d.counter_bytes = counter_bytes;
   d.events = ev;
   r->draw_next = (r->draw_next + 1) % kDrawRing;
   r->frame_index += n;
@@ -1369,6 +1433,7 @@ int mrt_renderer_destroy(mrt_renderer* r) {
   if (r->own_image && r->image) (void)hipFree(r->image);
   for (FrameSlot& fs : r->slots) {
     if (fs.acc_done) (void)hipEventDestroy(fs.acc_done);
+    if (fs.kernel_done) (void)hipEventDestroy(fs.kernel_done);
     if (fs.own_stream) (void)hipStreamDestroy(fs.stream);
   }
   r->slots.clear();
@@ -1376,7 +1441,9 @@ int mrt_renderer_destroy(mrt_renderer* r) {
     for (hipEvent_t e : d.kernel_events) (void)hipEventDestroy(e);
     if (d.start) (void)hipEventDestroy(d.start);
     if (d.stop) (void)hipEventDestroy(d.stop);
+    if (d.cleared) (void)hipEventDestroy(d.cleared);
   }
+  if (r->readback) (void)hipStreamDestroy(r->readback);
   if (r->own_stream) (void)hipStreamDestroy(r->stream);
   delete r;
   return MRT_OK;

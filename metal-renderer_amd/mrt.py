@@ -114,7 +114,8 @@ class Stats(ctypes.Structure):
         ("frame_index", ctypes.c_uint64), ("paths", ctypes.c_uint64), ("active_ray_bounces", ctypes.c_uint64),
         ("last_draw_ms", ctypes.c_double), ("mpaths_per_s", ctypes.c_double),
         ("kernel_launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("owned_pixels", ctypes.c_uint64),
-        ("timed_launches", ctypes.c_uint64), ("kernel", ctypes.c_uint32),
+        ("timed_launches", ctypes.c_uint64), ("kernel", ctypes.c_uint32), ("inflight", ctypes.c_uint32),
+        ("span_ms", ctypes.c_double), ("spans", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -145,6 +145,65 @@ def test_frames_in_flight_bitwise(gpu, mrt_mod, monkeypatch, inflight):
         assert a[0].tobytes() == b[0].tobytes() and a[1] == b[1], scene
 
 
+@pytest.mark.parametrize("scene,L", [("cornellbox", 4), ("CornellBox-Water-plastic", 8)])
+def test_pipelined_tile_share_bitwise(gpu, mrt_mod, monkeypatch, scene, L):
+    """A tile share renders on two streams by default (batch b + 1, of this
+    draw or the next, starts while batch b drains; accumulates in order on
+    the main stream): draws, a reset, more draws and a resize must give the
+    single-stream image and counts bitwise."""
+    sc = mrt_mod.Scene(scene)
+    out = {}
+    for k in (None, "1"):
+        if k is None:
+            monkeypatch.delenv("MRT_INFLIGHT", raising=False)
+        else:
+            monkeypatch.setenv("MRT_INFLIGHT", k)
+        monkeypatch.setenv("MRT_BATCH", "3")
+        r = mrt_mod.Renderer(sc, 200, 136, L, shard_rank=1, shard_count=3)
+        imgs = []
+        r.draw(7)
+        r.draw(4)
+        imgs.append(r.read_image())
+        r.reset()
+        for _ in range(3):
+            r.draw(2)
+        imgs.append(r.read_image())
+        r.resize(130, 70)
+        r.draw(5)
+        imgs.append(r.read_image())
+        out[k] = (imgs, r.stats()["active_ray_bounces"])
+        r.close()
+    (a, na), (b, nb) = out[None], out["1"]
+    assert na == nb
+    for x, y in zip(a, b):
+        assert np.isfinite(x).all() and x[..., :3].max() > 0
+        assert x.tobytes() == y.tobytes()
+
+
+def test_device_spans_match_events(gpu, mrt_mod):
+    """Every frame batch's render launch records its device span (earliest
+    block start to latest wave end, the chip's wall clock); with one render
+    stream the HIP events around the launch bracket the same span, so the
+    two timings agree (events include the launch latency: >= span)."""
+    sc = mrt_mod.Scene("cornellbox")
+    r = mrt_mod.Renderer(sc, 960, 540, 4, profile=True)
+    r.draw(16)
+    r.sync()
+    r.reset()
+    st0 = r.stats()
+    for _ in range(3):
+        r.draw(16)
+    r.sync()
+    st = r.stats()
+    r.close()
+    assert st["inflight"] == 1
+    spans, timed = st["spans"] - st0["spans"], st["timed_launches"] - st0["timed_launches"]
+    assert spans == 3 and timed == 3
+    span_ms = (st["span_ms"] - st0["span_ms"]) / spans
+    event_ms = (st["kernel_ms"] - st0["kernel_ms"]) / timed
+    assert 0.0 < span_ms <= event_ms * 1.01 and span_ms >= 0.8 * event_ms, (span_ms, event_ms)
+
+
 @pytest.mark.parametrize("build", ["precise", "fast"])
 def test_path_kernel_equals_wavefront(gpu, mrt_mod, monkeypatch, tmp_path, build):
     """The path megakernel (the product's kernel for scenes traversed from

@@ -49,12 +49,18 @@ def main(tag="r1", cfg="c2"):
     write, _ = counters(os.path.join(src, "write", "run_counter_collection.csv"))
     sq, _ = counters(os.path.join(src, "sq", "run_counter_collection.csv"))
     clk, _ = counters(os.path.join(src, "clk", "run_counter_collection.csv"))
+    lanes_csv = os.path.join(src, "lanes", "run_counter_collection.csv")
+    lanes = counters(lanes_csv)[0] if os.path.exists(lanes_csv) else {}
+    # VALUUtilization (rocprofiler-sdk counter_defs.yaml): active lanes per
+    # issued VALU instruction / 64 — the share of issued lane-slots doing work
+    lane_util = (lanes["SQ_THREAD_CYCLES_VALU"] / (64.0 * lanes["SQ_ACTIVE_INST_VALU"])
+                 if lanes.get("SQ_ACTIVE_INST_VALU") else None)
     bounce = next(r for r in rows if any(k in r["Name"] for k in HOT))
     avg_ns = float(bounce["AverageNs"])
     hbm = (2.0 * fetch["FETCH_SIZE"] + write["WRITE_SIZE"]) * 1024.0
     lines = [f"# rocprofv3 summary — {tag} / {cfg}", "",
              "`tools/profile.sh` → kernel trace + stats pass, then separate PMC passes "
-             "(FETCH_SIZE; WRITE_SIZE; SQ; GRBM), `bench.py --steps 2 --warmup 1`.", "",
+             "(FETCH_SIZE; WRITE_SIZE; SQ; VALU lanes; GRBM), `bench.py --steps 2 --warmup 1`.", "",
              "| kernel | calls | avg µs | total ms | % |", "|---|---|---|---|---|"]
     for r in rows:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
@@ -82,6 +88,9 @@ def main(tag="r1", cfg="c2"):
         commit = None
     lines.append(f"* VALU issue share = 2 x VALU insts / (1024 SIMDs x clock x launch) = "
                  f"{valu_frac if valu_frac is None else round(valu_frac, 3)}")
+    if lane_util is not None:
+        lines.append(f"* VALU lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) = {lane_util:.3f} "
+                     f"(share of issued lane-slots with an active lane)")
     md5_path = os.path.join(src, "lib.md5")
     lib_md5 = open(md5_path).read().strip() if os.path.exists(md5_path) else None
     m = re.search(r"(bounce_\w*kernel|path_kernel|stream_kernel)<[^>]*>", bounce["Name"])
@@ -97,7 +106,8 @@ def main(tag="r1", cfg="c2"):
                    "sq": sq, "clock_ghz": round(clk_hz / 1e9, 3),
                    "valu_issue_frac": None if valu_frac is None else round(valu_frac, 4),
                    "wait_any_frac": round(sq.get("SQ_WAIT_ANY", 0) / wave_cycles, 4),
-                   "valu_active_frac": round(sq.get("SQ_ACTIVE_INST_VALU", 0) / wave_cycles, 4)},
+                   "valu_active_frac": round(sq.get("SQ_ACTIVE_INST_VALU", 0) / wave_cycles, 4),
+                   "valu_lane_util": None if lane_util is None else round(lane_util, 4), "lanes": lanes},
                   f, indent=1)
     print("\n".join(lines))
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 passes for one bench config (run on the GPU box from the repo root).
 # usage: tools/profile.sh <tag> <config> [extra bench args]
-# pass 1: kernel trace + stats; passes 2-4: PMC counters, each in its own run
+# pass 1: kernel trace + stats; passes 2-6: PMC counters, each in its own run
 # (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).
 TAG=${1:-r1}; CFG=${2:-c2}; shift 2
 export TMPDIR=/tmp
@@ -16,4 +16,5 @@ step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -f csv -- $
 step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/fetch -o run -f csv -- $BENCH
 step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/write -o run -f csv -- $BENCH
 step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/sq -o run -f csv -- $BENCH
+step lanes 400 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/lanes -o run -f csv -- $BENCH
 step clk 400 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/clk -o run -f csv -- $BENCH
