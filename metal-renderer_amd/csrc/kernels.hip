@@ -460,9 +460,9 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 #ifndef MRT_PATH_SLACK   // trav_round(): the path kernel
 #define MRT_PATH_SLACK 12
 #endif
-#ifndef MRT_LEAF_SLACK   // trav_round(): the leaf loop's (a kept leaf is tested next round)
-#define MRT_LEAF_SLACK 0
-#endif
+#ifndef MRT_LEAF_SLACK   // trav_round(): the leaf loop's (a kept leaf is tested next round):
+#define MRT_LEAF_SLACK 8 // with path slack 12, C4 2480 -> 2645 (+6.7 %), C3 2340 -> 2474 (+5.7 %);
+#endif                   // 2 / 4 / 12 / 16 / 24 / 32: C4 2577 / 2605 / 2645 / 2640 / 2623 / 2611
 
 template <int STACK>
 __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {

@@ -108,6 +108,9 @@ struct DrawRecord {
                                             // counters (one buffer: one memset per draw)
   hipEvent_t start = nullptr, stop = nullptr;
   hipEvent_t cleared = nullptr;             // the counters' memset (other render streams of the draw wait on it)
+  hipEvent_t copied = nullptr;              // the counters' copy to `host` (read-back stream) is done
+  void* host = nullptr;                     // pinned copy of `counters`, queued behind the draw
+  size_t host_bytes = 0;
   std::vector<hipEvent_t> kernel_events;    // MRT_FLAG_PROFILE: 2 per timed bounce launch
   uint32_t frames = 0;
   uint32_t launches = 0;                    // batches (bounce launches = batches * L)
@@ -182,7 +185,6 @@ struct mrt_renderer {
   // launches 2.1-ms kernels, where that drain is 10 %.
   uint32_t inflight = 1;
   uint32_t slot_next = 0;   // slot of the next batch (rotates across draws)
-  hipStream_t readback = nullptr;   // draw statistics read-back (never waits for queued work)
   double wall_khz = 0.0;    // device wall clock (span timestamps; 0 = spans off, MRT_SPANS=0)
   bool image_foreign = false;   // the image holds pixels this renderer did not render (exchange / tiles_write)
   uint32_t grid = 0;        // persistent grid of the bounce kernel
@@ -216,13 +218,11 @@ int finalize_draw(mrt_renderer* r, DrawRecord& d) {
   float ms = 0.0f;
   HIP_TRY(hipEventElapsedTime(&ms, d.start, d.stop));
   const uint32_t L = r->desc.max_path_length;
-  // one copy of the whole counter buffer (survivor counts, grab counters,
-  // spans) on the renderer's private read-back stream: the draw is complete
-  // (its stop event has fired), and nothing queued after it is waited for
-  std::vector<uint32_t> buf((d.counter_bytes + 3) / 4);
-  HIP_TRY(hipMemcpyAsync(buf.data(), d.counters.p, d.counter_bytes, hipMemcpyDeviceToHost, r->readback));
-  HIP_TRY(hipStreamSynchronize(r->readback));
-  const uint32_t* cnt = buf.data();
+  // the whole counter buffer (survivor counts, grab counters, spans) was
+  // copied to pinned memory on the main stream behind the draw: no
+  // synchronous copy, so the host never waits for work queued after it
+  HIP_TRY(hipEventSynchronize(d.copied));
+  const uint32_t* cnt = static_cast<const uint32_t*>(d.host);
   uint64_t active = r->owned_pixels * d.frames;   // bounce 0: every owned pixel's camera ray
   for (uint32_t k = 0; k < d.launches; ++k)
     for (uint32_t b = 0; b + 1 < L; ++b) active += cnt[(size_t)k * L + b];
@@ -233,7 +233,7 @@ int finalize_draw(mrt_renderer* r, DrawRecord& d) {
   r->stats.kernel_launches += (uint64_t)d.launches * (r->path_mode || r->stream_mode ? 1u : L);
   {
     std::vector<unsigned long long> sp((size_t)2 * d.launches);
-    std::memcpy(sp.data(), reinterpret_cast<const char*>(buf.data()) + d.span_off, sp.size() * 8);
+    std::memcpy(sp.data(), static_cast<const char*>(d.host) + d.span_off, sp.size() * 8);
     for (uint32_t k = 0; k < d.launches; ++k) {
       const unsigned long long t0 = ~sp[2 * k], t1 = sp[2 * k + 1];
       if (sp[2 * k] && t1 >= t0 && r->wall_khz > 0.0) {
@@ -1082,6 +1082,7 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     HIP_TRY(hipEventCreate(&d.start));
     HIP_TRY(hipEventCreate(&d.stop));
     HIP_TRY(hipEventCreateWithFlags(&d.cleared, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
   }
   // LDS stack capacity: the BVH's bound rounded up to 8/16 entries when it is
   // <= 16; deeper BVHs keep 8 entries in LDS and spill the rest to global
@@ -1103,7 +1104,6 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, desc->scene->device) == hipSuccess)
       r->wall_khz = (double)khz;
   }
-  HIP_TRY(hipStreamCreateWithFlags(&r->readback, hipStreamNonBlocking));
   if (const char* v = std::getenv("MRT_SPANS"))
     if (std::atoi(v) == 0) r->wall_khz = 0.0;
   r->inflight = S > 1 ? 2u : 1u;
@@ -1303,6 +1303,17 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   }
   r->slot_next = (s0 + nb) % r->inflight;
   HIP_TRY(hipEventRecord(d.stop, r->stream));
+  if (d.host_bytes < counter_bytes) {
+    if (d.host) HIP_TRY(hipHostFree(d.host));
+    d.host = nullptr;
+    d.host_bytes = 0;
+    HIP_TRY(hipHostMalloc(&d.host, counter_bytes, hipHostMallocDefault));
+    d.host_bytes = counter_bytes;
+  }
+  // (no stream of its own: a process has few hardware queues — 4 by
+  // default — and two streams sharing one serialise their launches)
+  HIP_TRY(hipMemcpyAsync(d.host, d.counters.p, counter_bytes, hipMemcpyDeviceToHost, r->stream));
+  HIP_TRY(hipEventRecord(d.copied, r->stream));
   d.pending = true;
   d.frames = n;
   d.launches = nb;
@@ -1442,8 +1453,9 @@ int mrt_renderer_destroy(mrt_renderer* r) {
     if (d.start) (void)hipEventDestroy(d.start);
     if (d.stop) (void)hipEventDestroy(d.stop);
     if (d.cleared) (void)hipEventDestroy(d.cleared);
+    if (d.copied) (void)hipEventDestroy(d.copied);
+    if (d.host) (void)hipHostFree(d.host);
   }
-  if (r->readback) (void)hipStreamDestroy(r->readback);
   if (r->own_stream) (void)hipStreamDestroy(r->stream);
   delete r;
   return MRT_OK;
