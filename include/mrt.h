@@ -268,6 +268,18 @@ int mrt_renderer_load_reference(mrt_renderer* r, const char* path);
  * accumulation image (tone map / sRGB / compare mode against the loaded
  * reference) into host memory (rgba: W*H*4 floats, row 0 = bottom). */
 int mrt_renderer_display(mrt_renderer* r, uint32_t flags, float compare_scale, float* rgba, size_t count);
+/* The same blit without a host wait, for a frame loop that keeps frames in
+ * flight as the reference does (MaxBuffersInFlight = 3, its semaphore:
+ * renderer/Renderer.mm:16,593-600).  _enqueue queues the blit of the image
+ * as of the draws queued so far, and its copy into display slot `slot`
+ * (< MRT_DISPLAY_SLOTS; pinned host memory owned by the renderer), on the
+ * renderer's stream, and returns at once.  _map waits for that slot's copy
+ * and returns its pixels (W*H*4 floats, row 0 = bottom), valid until the
+ * slot is enqueued again or the renderer is resized or destroyed.  Typical
+ * loop: draw; enqueue(frame % 3); present map((frame - 2) % 3). */
+#define MRT_DISPLAY_SLOTS 3u
+int mrt_renderer_display_enqueue(mrt_renderer* r, uint32_t flags, float compare_scale, uint32_t slot);
+int mrt_renderer_display_map(mrt_renderer* r, uint32_t slot, const float** rgba, size_t* count);
 
 /* Multi-GPU exchange of the accumulation image: a shard's
  * owned 64x64 tiles packed densely, [k][64*64] RGBA32F for its k-th owned

@@ -208,6 +208,12 @@ struct mrt_renderer {
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
   Exchange x;
   DevBuf reference, display;   // comparison image (mrt_renderer_load_reference) and blit output
+  struct DisplaySlot {          // mrt_renderer_display_enqueue / _map: pinned copies of the blit
+    float* host = nullptr;
+    size_t floats = 0;
+    hipEvent_t done = nullptr;
+    bool queued = false;
+  } shown[MRT_DISPLAY_SLOTS];
 };
 
 namespace {
@@ -1424,6 +1430,46 @@ int mrt_renderer_display(mrt_renderer* r, uint32_t flags, float compare_scale, f
   return mrt_renderer_sync(r);
 }
 
+int mrt_renderer_display_enqueue(mrt_renderer* r, uint32_t flags, float compare_scale, uint32_t slot) {
+  if (!r) return fail(MRT_ERR_INVALID, "null renderer");
+  if (slot >= MRT_DISPLAY_SLOTS) return fail(MRT_ERR_INVALID, "display slot >= MRT_DISPLAY_SLOTS");
+  if (((flags >> 8) & 0xFFu) && !r->reference.p) return fail(MRT_ERR_STATE, "compare mode without a loaded reference");
+  const size_t need = (size_t)r->desc.width * r->desc.height * 4;
+  auto& ds = r->shown[slot];
+  if (ds.queued) HIP_TRY(hipEventSynchronize(ds.done));   // its previous copy may still be landing
+  if (ds.floats != need) {
+    if (ds.host) HIP_TRY(hipHostFree(ds.host));
+    ds.host = nullptr;
+    ds.floats = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ds.host), need * 4, hipHostMallocDefault));
+    ds.floats = need;
+  }
+  if (!ds.done) HIP_TRY(hipEventCreateWithFlags(&ds.done, hipEventDisableTiming));
+  int rc = exchange_flush(r);
+  if (rc) return rc;
+  // one device blit buffer: the next blit is queued behind this copy
+  if (r->display.bytes < need * 4) HIP_TRY(r->display.alloc(need * 4));
+  rc = mrt_display(r->image, r->reference.as<float>(), r->display.as<float>(), r->desc.width, r->desc.height, flags,
+                   compare_scale, r->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(ds.host, r->display.p, need * 4, hipMemcpyDeviceToHost, r->stream));
+  HIP_TRY(hipEventRecord(ds.done, r->stream));
+  ds.queued = true;
+  return MRT_OK;
+}
+
+int mrt_renderer_display_map(mrt_renderer* r, uint32_t slot, const float** rgba, size_t* count) {
+  if (!r || !rgba) return fail(MRT_ERR_INVALID, "null argument");
+  if (slot >= MRT_DISPLAY_SLOTS) return fail(MRT_ERR_INVALID, "display slot >= MRT_DISPLAY_SLOTS");
+  auto& ds = r->shown[slot];
+  if (!ds.queued || ds.floats != (size_t)r->desc.width * r->desc.height * 4)
+    return fail(MRT_ERR_STATE, "display slot not enqueued at the current size");
+  HIP_TRY(hipEventSynchronize(ds.done));
+  *rgba = ds.host;
+  if (count) *count = ds.floats;
+  return MRT_OK;
+}
+
 int mrt_renderer_stats(const mrt_renderer* r, mrt_stats* stats) {
   if (!r || !stats) return fail(MRT_ERR_INVALID, "null argument");
   int rc = finalize_pending(const_cast<mrt_renderer*>(r));
@@ -1442,6 +1488,10 @@ int mrt_renderer_destroy(mrt_renderer* r) {
     if (r->x.gather_done[i]) (void)hipEventDestroy(r->x.gather_done[i]);
   }
   if (r->own_image && r->image) (void)hipFree(r->image);
+  for (auto& ds : r->shown) {
+    if (ds.done) (void)hipEventDestroy(ds.done);
+    if (ds.host) (void)hipHostFree(ds.host);
+  }
   for (FrameSlot& fs : r->slots) {
     if (fs.acc_done) (void)hipEventDestroy(fs.acc_done);
     if (fs.kernel_done) (void)hipEventDestroy(fs.kernel_done);

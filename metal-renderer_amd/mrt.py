@@ -136,6 +136,7 @@ EXPORTED = [
     "mrt_comm_unique_id", "mrt_comm_create", "mrt_comm_destroy", "mrt_renderer_exchange",
     "mrt_renderer_exchange_flush", "mrt_renderer_tiles_read", "mrt_renderer_tiles_write",
     "mrt_image_load_exr", "mrt_renderer_load_reference", "mrt_renderer_display",
+    "mrt_renderer_display_enqueue", "mrt_renderer_display_map",
 ]
 
 _lib = None
@@ -209,6 +210,8 @@ def lib() -> ctypes.CDLL:
         "mrt_image_load_exr": [ctypes.c_char_p, vp, ctypes.c_size_t, ctypes.POINTER(u32), ctypes.POINTER(u32)],
         "mrt_renderer_load_reference": [vp, ctypes.c_char_p],
         "mrt_renderer_display": [vp, u32, ctypes.c_float, vp, ctypes.c_size_t],
+        "mrt_renderer_display_enqueue": [vp, u32, ctypes.c_float, u32],
+        "mrt_renderer_display_map": [vp, u32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -429,6 +432,19 @@ class Renderer:
         _check(lib().mrt_renderer_display(self._h, flags, compare_scale, ctypes.c_void_p(img.ctypes.data), img.size),
                "mrt_renderer_display")
         return img
+
+    def display_enqueue(self, slot: int, flags: int = 0, compare_scale: float = 10.0) -> None:
+        """Queue the blit of the image into display slot `slot` (no host wait)."""
+        _check(lib().mrt_renderer_display_enqueue(self._h, flags, compare_scale, slot), "mrt_renderer_display_enqueue")
+
+    def display_map(self, slot: int):
+        """[H, W, 4] float32 copy of display slot `slot` (waits for its blit)."""
+        import numpy as np
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().mrt_renderer_display_map(self._h, slot, ctypes.byref(p), ctypes.byref(n)),
+               "mrt_renderer_display_map")
+        buf = (ctypes.c_float * n.value).from_address(p.value)
+        return np.frombuffer(buf, np.float32).reshape(self.height, self.width, 4).copy()
 
     def stats(self) -> dict:
         s = Stats()

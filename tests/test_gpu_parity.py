@@ -436,3 +436,35 @@ def test_c_cli_two_ranks_host_exchange(gpu, mrt_mod, tmp_path):
         assert p.returncode == 0, p.stderr
         imgs.append((tmp_path / name).read_bytes())
     assert imgs[0] == imgs[1]
+
+
+def test_display_ring_frames_in_flight(gpu, mrt_mod):
+    """The facade's frame loop (integration/objc/Renderer.mm): draw, enqueue
+    the blit of frame n into slot n % 3, map the slot of frame n - 2 — the
+    reference's 3 frames in flight.  Each mapped slot equals the synchronous
+    blit of the same frame, bitwise; misuse fails loudly."""
+    sc = _scene(mrt_mod, "cornellbox")
+    flags = 3   # tone map + sRGB
+    want = []
+    r = mrt_mod.Renderer(sc, 160, 120, 4)
+    for n in range(6):
+        r.draw()
+        want.append(r.display(flags, 10.0))
+    r.close()
+    r = mrt_mod.Renderer(sc, 160, 120, 4)
+    got = {}
+    for n in range(6):
+        r.draw()
+        r.display_enqueue(n % 3, flags, 10.0)
+        if n >= 2:
+            got[n - 2] = r.display_map((n - 2) % 3)
+    got[4], got[5] = r.display_map(4 % 3), r.display_map(5 % 3)
+    for n in range(6):
+        assert got[n].tobytes() == want[n].tobytes(), n
+    with pytest.raises(mrt_mod.MrtError, match="slot"):
+        r.display_enqueue(3)
+    r.resize(80, 64)
+    with pytest.raises(mrt_mod.MrtError, match="not enqueued"):
+        r.display_map(0)
+    r.close()
+

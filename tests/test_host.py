@@ -40,7 +40,9 @@ def test_objc_facade_binds_only_declared_symbols(mrt_mod):
     header = open(os.path.join(ROOT, "include", "mrt.h")).read()
     called = set(re.findall(r"\b(mrt_\w+)\s*\(", src))
     assert {"mrt_scene_create", "mrt_renderer_create", "mrt_renderer_resize", "mrt_renderer_draw",
-            "mrt_renderer_display", "mrt_renderer_load_reference", "mrt_renderer_save_image"} <= called
+            "mrt_renderer_display_enqueue", "mrt_renderer_display_map", "mrt_renderer_load_reference",
+            "mrt_renderer_save_image"} <= called
+    assert "mrt_renderer_display(" not in src   # no per-frame host wait (3 frames in flight)
     assert called <= set(mrt_mod.EXPORTED), called - set(mrt_mod.EXPORTED)
     for macro in set(re.findall(r"\b(MRT_[A-Z_]+)\b", src)):
         assert re.search(r"(#define\s+" + macro + r"|^\s*" + macro + r"\s*=)", header, re.M), macro
