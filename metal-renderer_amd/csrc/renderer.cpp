@@ -1095,8 +1095,11 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   // memory (MRT_STACK overrides the cap).  LDS per block bounds the resident
   // blocks per CU, and for global-memory traversal occupancy wins: C4 with
   // 8 LDS entries + spill ran 1.5x faster than with a 32-entry LDS stack.
+  // r3, with traversal slack: trees deeper than 32 entries (the 1M-triangle
+  // scenes, 48) keep 12 in LDS — C4 +1.9 %; C3 (26) is best at 8 (12: -0.4 %,
+  // C3g -0.9 %), and 16 entries lose everywhere (C4 -0.4 %, C3g -2.4 %)
   const uint32_t need = desc->scene->bvh.max_stack;
-  uint32_t cap = need <= 16 ? 16 : 8;
+  uint32_t cap = need <= 16 ? 16 : (need > 32 ? 12 : 8);
   if (const char* v = std::getenv("MRT_STACK")) cap = std::max<uint32_t>(8, (uint32_t)std::strtoul(v, nullptr, 0));
   const uint32_t want = std::min(need, cap);
   r->stack_entries = want <= 8 ? 8 : want <= 12 ? 12 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
