@@ -1595,11 +1595,19 @@ int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
   if (overlap) {
     // the collective waits for the pack (and, on rank 0, for the previous
     // unpack, which precedes the pack on the renderer's stream) and runs on
-    // the communicator's stream while the renderer's next draw proceeds
-    HIP_TRY(hipEventRecord(x.pack_done[i], r->stream));
-    HIP_TRY(hipStreamWaitEvent(c->stream, x.pack_done[i], 0));
-    NCCL_TRY(ncclGather(x.packed[i].p, recv, x.slab_floats, ncclFloat, 0, c->comm, c->stream));
-    HIP_TRY(hipEventRecord(x.gather_done[i], c->stream));
+    // the communicator's stream while the renderer's next draw proceeds.  A
+    // renderer with frame batches on two render streams (a tile share) never
+    // makes a render launch wait on its main stream, so there the collective
+    // stays on the main stream: a process has 4 hardware queues by default,
+    // and a stream sharing one with a render stream would hold that stream's
+    // launches behind the collective.
+    hipStream_t gs = r->inflight > 1 ? r->stream : c->stream;
+    if (gs != r->stream) {
+      HIP_TRY(hipEventRecord(x.pack_done[i], r->stream));
+      HIP_TRY(hipStreamWaitEvent(gs, x.pack_done[i], 0));
+    }
+    NCCL_TRY(ncclGather(x.packed[i].p, recv, x.slab_floats, ncclFloat, 0, c->comm, gs));
+    HIP_TRY(hipEventRecord(x.gather_done[i], gs));
     x.gather_recorded[i] = true;
     x.pending = i;
     return MRT_OK;

@@ -39,8 +39,14 @@ def _render(mrt_mod, sc, W, H, L, frames, steps, comm=None, mode=0, shard=(0, 1)
     return img
 
 
+@pytest.mark.parametrize("inflight", ["1", "2"])
 @pytest.mark.parametrize("mode", ["gather", "gather_overlap", "reduce"])
-def test_rccl_exchange_single_rank(gpu, mrt_mod, mode):
+def test_rccl_exchange_single_rank(gpu, mrt_mod, monkeypatch, mode, inflight):
+    """A 1-rank communicator: the exchange leaves the image bitwise as is.
+    inflight 2 (a tile share's default: render launches on two streams) runs
+    the overlapped gather on the renderer's main stream instead of the
+    communicator's."""
+    monkeypatch.setenv("MRT_INFLIGHT", inflight)
     sc = mrt_mod.Scene("cornellbox")
     W, H, L, frames = 200, 136, 4, 3
     ref = _render(mrt_mod, sc, W, H, L, frames, 1)
