@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 4
+#define MRT_ABI_VERSION 5
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -196,6 +196,9 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
   double span_ms;                  /* summed device-measured spans of the frame batches' render launches
                                       (earliest block start to latest wave end, chip wall clock) */
   uint64_t spans;                  /* frame batches behind span_ms (every batch) */
+  uint32_t primary_blocks;         /* 8x8 pixel blocks whose camera rays test a candidate list instead of
+                                      traversing the BVH (0 = lists off; MRT_PRIMARY=0 disables) */
+  float primary_mean;              /* mean candidate-list length over those blocks */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);

@@ -96,6 +96,8 @@ struct BounceArgs {
   uint32_t* bounce_counts;     // path / stream kernel: [max_path_length] rays alive at the start of bounce b + 1
   unsigned long long* span;    // [2] of the frame batch, zeroed: ~(earliest block start), latest wave end
                                // (wall_clock64 ticks; null = not recorded)
+  const uint32_t* primary;     // camera-ray candidate lists per 8x8 pixel block (primary.h; null = traverse)
+  uint32_t primary_bx;         // blocks per row of `primary`
 };
 
 // running-mean accumulation of one frame over the owned tiles

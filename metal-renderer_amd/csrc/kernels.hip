@@ -547,40 +547,68 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
 // lowest primitive index; (u, v) to uv[0], uv[kBlock] when uv is non-null).
 // Occlusion (any = true): true at the first primitive k != target with
 // (t_k, k) < (h.t, target).
+// Leaf-ordered triangles ka and kb (kb tested only when `pair`), both loaded
+// before either test.
+template <int MODE>
+__device__ __forceinline__ bool tri_pair(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
+                                         uint32_t ka, uint32_t kb, bool pair, Hit& h, bool any, uint32_t target,
+                                         uint32_t* uv) {
+  float4 a0, a1, a2, b0, b1, b2;
+  fetch_tri<MODE>(sc, cx, ka, a0, a1, a2);
+  fetch_tri<MODE>(sc, cx, kb, b0, b1, b2);
+  float t[2], u[2], v[2];
+  bool ok[2];
+  ok[0] = tri_bary(o, d, mk(a0), mk(a1), mk(a2), t[0], u[0], v[0]);
+  ok[1] = tri_bary(o, d, mk(b0), mk(b1), mk(b2), t[1], u[1], v[1]) & pair;
+  const uint32_t prim[2] = {fbits(a0.w), fbits(b0.w)};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const bool hit = ok[j] & (t[j] >= tmin) & (t[j] <= h.t);
+    if (any) {
+      if (hit & (prim[j] != target) & ((t[j] < h.t) | (prim[j] < target))) return true;
+    } else if (hit & (!h.found | (t[j] < h.t) | (prim[j] < h.prim))) {
+      h.found = true;
+      h.t = t[j];
+      if (uv) {
+        uv[0] = fbits(u[j]);
+        uv[kBlock] = fbits(v[j]);
+      } else {
+        h.u = u[j];
+        h.v = v[j];
+      }
+      h.prim = prim[j];
+    }
+  }
+  return false;
+}
+
 template <int MODE>
 __device__ __forceinline__ bool leaf_tests(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
                                            uint32_t first, uint32_t cnt, Hit& h, bool any, uint32_t target,
                                            uint32_t* uv) {
   for (uint32_t k = 0; k < cnt; k += 2) {
     const uint32_t k1 = min(k + 1, cnt - 1);
-    float4 a0, a1, a2, b0, b1, b2;
-    fetch_tri<MODE>(sc, cx, first + k, a0, a1, a2);
-    fetch_tri<MODE>(sc, cx, first + k1, b0, b1, b2);
-    float t[2], u[2], v[2];
-    bool ok[2];
-    ok[0] = tri_bary(o, d, mk(a0), mk(a1), mk(a2), t[0], u[0], v[0]);
-    ok[1] = tri_bary(o, d, mk(b0), mk(b1), mk(b2), t[1], u[1], v[1]) & (k1 != k);
-    const uint32_t prim[2] = {fbits(a0.w), fbits(b0.w)};
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bool hit = ok[j] & (t[j] >= tmin) & (t[j] <= h.t);
-      if (any) {
-        if (hit & (prim[j] != target) & ((t[j] < h.t) | (prim[j] < target))) return true;
-      } else if (hit & (!h.found | (t[j] < h.t) | (prim[j] < h.prim))) {
-        h.found = true;
-        h.t = t[j];
-        if (uv) {
-          uv[0] = fbits(u[j]);
-          uv[kBlock] = fbits(v[j]);
-        } else {
-          h.u = u[j];
-          h.v = v[j];
-        }
-        h.prim = prim[j];
-      }
-    }
+    if (tri_pair<MODE>(sc, cx, o, d, tmin, first + k, first + k1, k1 != k, h, any, target, uv)) return true;
   }
   return false;
+}
+
+// Camera rays of one 8x8 pixel block through the block's candidate list
+// (primary.h): the nearest hit over the listed triangles with the leaf test's
+// arithmetic and tie rule — the traversal's answer, since the list holds
+// every triangle a ray of the block can hit.  `list` / `cnt` are
+// wave-uniform (scalar loads; LDS-resident triangles are broadcast reads).
+template <int MODE>
+__device__ __forceinline__ void primary_nearest(const DeviceScene& sc, const LdsCtx& cx, const uint32_t* list,
+                                                uint32_t cnt, V3 o, V3 d, Hit& h) {
+  h.t = __builtin_inff();
+  h.u = h.v = 0.0f;
+  h.prim = 0xFFFFFFFFu;
+  h.found = false;
+  for (uint32_t j = 0; j < cnt; j += 2) {
+    const uint32_t j1 = min(j + 1, cnt - 1);
+    tri_pair<MODE>(sc, cx, o, d, 0.0f, list[j], list[j1], j1 != j, h, false, 0u, nullptr);
+  }
 }
 
 template <int STACK, int MODE, bool ANY>
@@ -1094,6 +1122,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   // -- phase 0: generate (bounce 0) or load (SoA queue planes 0-1) the ray
   PathState s;
   uint32_t tag = 0;   // tag = global owned slot | prevDiffuse << 31
+  uint32_t pblk = 0xFFFFFFFFu;   // bounce 0: the pixel's 8x8 block (camera-ray candidate lists)
   if (active) {
     if (bounce == 0) {
       // frame fj of the batch (num_slots is a multiple of 4096: waves never
@@ -1104,6 +1133,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
       active = (x < a.width) && (y < a.height);
       if (active) {
         tag = idx;
+        pblk = (x / kPrimaryBlock) + (y / kPrimaryBlock) * a.primary_bx;
         const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
         camera_ray(x, y, a.width, a.height, ns, s.o, s.d);
       }
@@ -1122,7 +1152,20 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   // -- phase 1: nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
   Hit h;
   h.found = false;
-  if (active) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+  bool listed = false;
+  if (bounce == 0 && a.primary) {
+    // a wave of camera rays is one 8x8 pixel block (slot_pixel): its
+    // candidate list, when every active lane is in the same block
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(pblk);
+    const bool uniform = b0 != 0xFFFFFFFFu && __ballot(active && pblk != b0) == 0;
+    const uint32_t hd = uniform ? __builtin_amdgcn_readfirstlane(a.primary[b0]) : kPrimaryFallback;
+    const uint32_t cnt = hd & 0xFFu;
+    if (cnt != kPrimaryFallback) {
+      listed = true;
+      if (active) primary_nearest<MODE>(sc, cx, a.primary + (hd >> 8), cnt, s.o, s.d, h);
+    }
+  }
+  if (active && !listed) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
   STAMP_AT(st, 1);
   // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
   //    near hit ends the path (:122-126)

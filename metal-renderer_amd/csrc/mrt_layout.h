@@ -99,6 +99,11 @@ struct DeviceScene {
   uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack)
 };
 
+// camera-ray candidate lists (primary.h): header (offset << 8) | count per
+// 8x8 pixel block; count kPrimaryFallback = traverse the BVH
+constexpr uint32_t kPrimaryFallback = 0xFFu;
+constexpr uint32_t kPrimaryBlock = 8;
+
 // float4s per node record of a BVH width
 #if defined(__HIPCC__)
 #define MRT_HD __host__ __device__

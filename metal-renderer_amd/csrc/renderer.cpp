@@ -29,6 +29,7 @@
 #include "image.h"
 #include "kernels.h"
 #include "noise.h"
+#include "primary.h"
 #include "scene.h"
 
 namespace {
@@ -206,6 +207,13 @@ struct mrt_renderer {
   bool stream_mode = false; // wavefront as one launch per frame batch with per-wave queues (stream_kernel)
   bool path_mode = true;   // one path-megakernel launch per frame batch (else L bounce launches, MRT_KERNEL=wave)
   uint32_t debug = 0;   // MRT_DEBUG ablation bits (profiling only)
+  // camera-ray candidate lists per 8x8 pixel block (primary.h), rebuilt for
+  // every frame size; the wavefront kernels' bounce 0 tests a block's list
+  // instead of traversing (MRT_PRIMARY=0: off, MRT_PRIMARY_CAP: longest list)
+  bool primary_allowed = true;
+  uint32_t primary_cap = 12;
+  DevBuf primary;
+  uint32_t primary_bx = 0;
   Exchange x;
   DevBuf reference, display;   // comparison image (mrt_renderer_load_reference) and blit output
   struct DisplaySlot {          // mrt_renderer_display_enqueue / _map: pinned copies of the blit
@@ -355,6 +363,19 @@ int alloc_frame_buffers(mrt_renderer* r) {
   r->stats.owned_pixels = r->owned_pixels;
   r->stats.kernel = r->path_mode ? 1u : (r->stream_mode ? 2u : 0u);
   r->stats.inflight = r->inflight;
+  {
+    mrt::PrimaryLists pl;
+    const mrt::BvhResult& b = r->scene->bvh;
+    HIP_TRY(r->primary.alloc(0));
+    r->primary_bx = 0;
+    if (r->primary_allowed && !r->path_mode &&
+        mrt::build_primary_lists(b.tris.data(), (uint32_t)(b.tris.size() / 12), W, H, r->primary_cap, pl)) {
+      HIP_TRY(upload(r->primary, pl.words.data(), pl.words.size() * 4));
+      r->primary_bx = pl.blocks_x;
+      r->stats.primary_blocks = pl.listed_blocks;
+      r->stats.primary_mean = (float)pl.mean_count;
+    }
+  }
   // the render streams do not wait on the main stream: its memsets above
   // (segments, image) complete before any batch is queued
   HIP_TRY(hipStreamSynchronize(r->stream));
@@ -1135,6 +1156,9 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   // wavefront), scenes staged whole in LDS the wavefront of per-bounce
   // launches (C2: the path kernel is 24 % slower); MRT_KERNEL=path|wave
   // overrides.
+  if (const char* v = std::getenv("MRT_PRIMARY")) r->primary_allowed = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MRT_PRIMARY_CAP"))
+    r->primary_cap = std::max<uint32_t>(1, std::min<uint32_t>(mrt::kPrimaryFallback - 1, (uint32_t)std::strtoul(v, nullptr, 0)));
   r->path_mode = mrt::fast::path_preferred(desc->scene->dev);
   if (const char* k = std::getenv("MRT_KERNEL")) r->path_mode = std::strcmp(k, "path") == 0;
   if (r->path_mode)
@@ -1278,6 +1302,8 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.radiance = fs.radiance.as<float4>();
       a.stack_spill = fs.spill.as<uint32_t>();
       a.bounce_counts = cnt + (size_t)k * L;
+      a.primary = r->primary.as<uint32_t>();
+      a.primary_bx = r->primary_bx;
       a.span = r->wall_khz > 0.0
                    ? reinterpret_cast<unsigned long long*>(static_cast<char*>(d.counters.p) + span_off) + 2 * k
                    : nullptr;

@@ -116,6 +116,7 @@ class Stats(ctypes.Structure):
         ("kernel_launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("owned_pixels", ctypes.c_uint64),
         ("timed_launches", ctypes.c_uint64), ("kernel", ctypes.c_uint32), ("inflight", ctypes.c_uint32),
         ("span_ms", ctypes.c_double), ("spans", ctypes.c_uint64),
+        ("primary_blocks", ctypes.c_uint32), ("primary_mean", ctypes.c_float),
     ]
 
     def as_dict(self):
