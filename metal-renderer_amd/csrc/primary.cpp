@@ -94,24 +94,26 @@ bool build_primary_lists(const float* tris, uint32_t num_tris, uint32_t W, uint3
     const D3 n = cross(e1, e2);
     const double nl = len(n), l1 = len(e1), l2 = len(e2);
     const double hgt = nl > 0.0 ? std::fabs(dot(n, sub(v0, O))) / nl : 0.0;   // camera's distance to the plane
-    bool all = smin < 1e-3 || !(nl > 1e-9 * l1 * l2) || !(hgt > 1e-3 * R);
+    bool all = smin < 1e-3 || !(nl > 1e-9 * l1 * l2) || !(hgt > 1e-7 * R);
     double m = kMargin;
     double p[3][2];
     if (!all) {
+      double pmax = 0.0;
       for (int i = 0; i < 3; ++i) {
         p[i][0] = rel[i].x / -rel[i].z;
         p[i][1] = rel[i].y / -rel[i].z;
+        pmax = std::max(pmax, std::fabs(p[i][0]) + std::fabs(p[i][1]));
       }
-      // |det| >= |n| hgt / R for every camera ray that meets the plane inside
-      // the triangle; the barycentric error of the float test is then at most
-      // ~ eps * max(|e|, R)^2 R / (|n| hgt) (generous constant), and it moves
-      // the projected edges by at most that times the projection's diameter
-      const double big = std::max({l1, l2, R});
-      const double db = 64.0 * kEps * big * big * R / (nl * hgt);
-      double diam = 0.0;
-      for (int i = 0; i < 3; ++i)
-        diam = std::max(diam, std::hypot(p[i][0] - p[(i + 1) % 3][0], p[i][1] - p[(i + 1) % 3][1]));
-      m += db * diam;
+      // Float error of the test (tri_bary: det = e1.(d x e2), b1 = (s.p)/det,
+      // b2 = (d.q)/det, s = o - v0 with |s| <= R): a camera ray meeting the
+      // plane at distance r <= R has |det| = |n| hgt / r >= |n| hgt / R, the
+      // numerators' rounding is ~eps R |e| and det's ~eps |e1||e2|, so a
+      // barycentric is off by at most db (generous constant).  That moves the
+      // hit point by db * |e|max in 3-D, at depth >= smin: at most
+      // db |e|max (1 + |p|) / smin on the image plane.
+      const double emax = std::max(l1, l2);
+      const double db = 16.0 * kEps * R * (R * emax + l1 * l2) / (nl * hgt);
+      m += 2.0 * db * emax * (1.0 + pmax) / smin;
       if (!(m < 0.25)) all = true;
     }
     if (all) {
