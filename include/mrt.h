@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 5
+#define MRT_ABI_VERSION 6
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -83,6 +83,9 @@ typedef struct mrt_scene_desc {
   int device;                      /* HIP device ordinal; -1 = host only (import + BVH, no upload) */
   uint32_t bvh_width;              /* 4 = BVH4 (the binary SAH tree collapsed), 0 = default (4); other widths are rejected */
   uint32_t bvh_builder;            /* MRT_BVH_*; 0 = default (host binned SAH) */
+  uint32_t no_occluder_tree;       /* 1: shadow rays always traverse the main tree (no occluder tree, see
+                                      mrt_scene_info.occluder_planes); 0 = default (built for host-SAH
+                                      scenes of <= 16384 triangles with culled supporting planes) */
 } mrt_scene_desc;
 
 /* BVH builders */
@@ -99,6 +102,12 @@ typedef struct mrt_scene_info {
   double bvh_sah_cost;
   double build_ms;                 /* host BVH build time */
   uint64_t device_bytes;           /* scene + BVH bytes resident on the device */
+  /* shadow-ray occluder tree: triangles in supporting planes with every light
+   * strictly inside (walls, floor, ceiling) cannot occlude a shadow ray from
+   * an origin inside those planes; such rays traverse a second BVH over the
+   * other triangles (same answers).  0 planes = no occluder tree. */
+  uint32_t occluder_planes, occluder_culled, occluder_nodes;
+  float occluder_margin;
 } mrt_scene_info;
 
 int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out);

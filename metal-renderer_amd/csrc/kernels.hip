@@ -279,12 +279,21 @@ __host__ __device__ constexpr uint32_t node_stride_f4(int mode, uint32_t node_f4
 }
 
 // float4 counts of the staged scene image for a mode
-// (node_f4 = float4s per BVH4 node: 8)
+// (node_f4 = float4s per BVH4 node: 8; nodes / tri_records include the
+// occluder tree's, prims are the scene's triangles)
 __host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t node_f4, uint32_t nodes, uint32_t lds_nodes,
-                                                      uint32_t tris, uint32_t mats, uint32_t lights) {
-  if (mode == kAllLds) return node_stride_f4(mode, node_f4) * nodes + 3 * tris + 6 * tris + 2 * mats + 7 * lights;
+                                                      uint32_t tri_records, uint32_t prims, uint32_t mats,
+                                                      uint32_t lights) {
+  if (mode == kAllLds) return node_stride_f4(mode, node_f4) * nodes + 3 * tri_records + 6 * prims + 2 * mats + 7 * lights;
   if (mode == kTopLds) return node_f4 * lds_nodes;
   return 0;
+}
+// both trees' nodes and leaf-triangle records (mrt_layout.h DeviceScene)
+__host__ __device__ inline uint32_t scene_nodes(const DeviceScene& sc) { return sc.num_nodes + sc.occ_nodes; }
+__host__ __device__ inline uint32_t scene_tri_records(const DeviceScene& sc) { return sc.num_triangles + sc.occ_tris; }
+__host__ __device__ inline uint32_t lds_scene_float4s(int mode, const DeviceScene& sc) {
+  return lds_scene_float4s(mode, node_float4s(sc.width), scene_nodes(sc), sc.lds_nodes, scene_tri_records(sc),
+                           sc.num_triangles, sc.num_materials, sc.num_lights + 1);
 }
 
 template <int MODE>
@@ -395,15 +404,16 @@ template <int MODE>
 __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scratch_u32, uint32_t* spill = nullptr) {
   LdsCtx cx;
   const uint32_t nf4 = node_float4s(sc.width);   // float4s per node
-  const uint32_t n_nodes = (MODE == kAllLds) ? sc.num_nodes : (MODE == kTopLds ? sc.lds_nodes : 0u);
-  const uint32_t T = (MODE == kAllLds) ? sc.num_triangles : 0u;
+  const uint32_t n_nodes = (MODE == kAllLds) ? scene_nodes(sc) : (MODE == kTopLds ? sc.lds_nodes : 0u);
+  const uint32_t TR = (MODE == kAllLds) ? scene_tri_records(sc) : 0u;   // leaf triangles of both trees
+  const uint32_t T = (MODE == kAllLds) ? sc.num_triangles : 0u;          // per-primitive records
   const uint32_t M = (MODE == kAllLds) ? sc.num_materials : 0u;
   const uint32_t NL = (MODE == kAllLds) ? sc.num_lights + 1 : 0u;
   cx.n_lds_nodes = n_nodes;
   const uint32_t node_f4 = node_stride_f4(MODE, nf4);
   const bool copies = node_f4 != nf4;
   cx.tri_base = node_f4 * n_nodes;
-  cx.prim_base = cx.tri_base + 3 * T;
+  cx.prim_base = cx.tri_base + 3 * TR;
   cx.mat_base = cx.prim_base + 6 * T;
   cx.light_base = cx.mat_base + 2 * M;
   const uint32_t f4 = cx.light_base + 7 * NL;
@@ -416,7 +426,7 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
                             reinterpret_cast<const float4*>(sc.prims), reinterpret_cast<const float4*>(sc.materials),
                             reinterpret_cast<const float4*>(sc.lights)};
     const uint32_t base[5] = {0u, cx.tri_base, cx.prim_base, cx.mat_base, cx.light_base};
-    const uint32_t len[5] = {nf4 * n_nodes, 3 * T, 6 * T, 2 * M, 7 * NL};
+    const uint32_t len[5] = {nf4 * n_nodes, 3 * TR, 6 * T, 2 * M, 7 * NL};
     for (int r = copies ? 1 : 0; r < 5; ++r)
       for (uint32_t i = threadIdx.x; i < len[r]; i += kBlock) g_lds[base[r] + i] = src[r][i];
     if (copies) {   // quadrant copies: x, y rows (near, far), z rows (lo, hi), refs
@@ -613,9 +623,9 @@ __device__ __forceinline__ void primary_nearest(const DeviceScene& sc, const Lds
 
 template <int STACK, int MODE, bool ANY>
 __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
-                                         uint32_t target) {
+                                         uint32_t target, int32_t root) {
   const RayBox rb = make_raybox(o, d);
-  int32_t node = sc.root, leaf = 0;
+  int32_t node = root, leaf = 0;
   int sp = 0;
   if (node < 0) { leaf = node; node = kDone; }
   while (node != kDone || leaf != 0) {
@@ -652,8 +662,22 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
-  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u);
+  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u, sc.root);
   return h;
+}
+
+// The tree a shadow ray from o traverses: the occluder tree when o is inside
+// every culled plane by the margin (occluders.h: no triangle of those planes
+// can then stand between o and a light), else the main tree.  The plane data
+// is wave-uniform (kernel argument, scalar registers).
+__device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o) {
+  if (sc.occ_planes == 0) return sc.root;
+  bool inside = true;
+  for (uint32_t k = 0; k < sc.occ_planes; ++k) {
+    const float* p = sc.occ_plane[k];
+    inside &= fmaf(p[0], o.x, fmaf(p[1], o.y, fmaf(p[2], o.z, -p[3]))) <= -sc.occ_margin;
+  }
+  return inside ? sc.occ_root : sc.root;
 }
 
 template <int STACK, int MODE>
@@ -662,7 +686,7 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
   Hit h;
   h.t = t_target;
   h.found = false;
-  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target);
+  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, shadow_root(sc, o));
 }
 
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
@@ -1498,8 +1522,8 @@ struct Trav {
   int32_t node, leaf;
   int sp;
 };
-__device__ __forceinline__ void trav_begin(const DeviceScene& sc, Trav& tr) {
-  tr.node = sc.root;
+__device__ __forceinline__ void trav_begin(int32_t root, Trav& tr) {
+  tr.node = root;
   tr.leaf = 0;
   tr.sp = 0;
   if (tr.node < 0) { tr.leaf = tr.node; tr.node = kDone; }
@@ -1642,7 +1666,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
           ps[11 * kBlock] = idx;   // prevDiffuse 0
           phase = 1;
           bounce = 0;
-          trav_begin(sc, tr);
+          trav_begin(sc.root, tr);
           h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
         }
       }
@@ -1725,7 +1749,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
             shadow = true;
             phase = 2;
             rd = sh.d;   // ro = s.o = sh.o
-            trav_begin(sc, tr);
+            trav_begin(shadow_root(sc, ro), tr);
             h.t = tT;
             h.u = sh.L.x;
             h.v = sh.L.y;
@@ -1745,7 +1769,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       // ro already holds the next ray's origin (set at shading, unchanged by a shadow query)
       rd = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
       phase = 1;
-      trav_begin(sc, tr);
+      trav_begin(sc.root, tr);
       h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
     }
   }
@@ -1899,15 +1923,13 @@ int choose_mode(const DeviceScene& sc) {
     return v ? std::atoi(v) : -1;
   }();
   if (forced >= 0 && forced <= 2) return forced;
-  if ((size_t)lds_scene_float4s(kAllLds, node_float4s(sc.width), sc.num_nodes, 0, sc.num_triangles, sc.num_materials,
-                                sc.num_lights + 1) * 16 <= kAllLdsBudget)
+  if ((size_t)lds_scene_float4s(kAllLds, sc) * 16 <= kAllLdsBudget)
     return kAllLds;
   return sc.lds_nodes > 0 ? kTopLds : kGlobal;
 }
 
 size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_t grid) {
-  const size_t scene = (size_t)lds_scene_float4s(mode, node_float4s(sc.width), sc.num_nodes, sc.lds_nodes,
-                                                 sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16;
+  const size_t scene = (size_t)lds_scene_float4s(mode, sc) * 16;
   const size_t scratch = ((size_t)2 * grid + 1 + 3) / 4 * 16;   // segment counts per block (2 classes) + sentinel
   return scene + scratch + (size_t)stack * kBlock * 4;           // stack = LDS entries (|STACK|)
 }
@@ -1964,8 +1986,7 @@ hipError_t grid_for(const DeviceScene& sc, uint32_t blocks_per_cu, uint32_t* gri
 // path kernel: LDS = scene image + stack + the per-lane path state; the
 // kTopLds node budget fits MRT_PATH_WAVES resident blocks per CU
 size_t path_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack) {
-  const size_t scene = (size_t)lds_scene_float4s(mode, node_float4s(sc.width), sc.num_nodes, sc.lds_nodes,
-                                                 sc.num_triangles, sc.num_materials, sc.num_lights + 1) * 16;
+  const size_t scene = (size_t)lds_scene_float4s(mode, sc) * 16;
   return scene + 16 + (size_t)stack * kBlock * 4 + (size_t)kPathStateWords * kBlock * 4;
 }
 DeviceScene fit_path_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack) {

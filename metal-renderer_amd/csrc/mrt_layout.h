@@ -96,8 +96,22 @@ struct DeviceScene {
   uint32_t num_lights;       // light triangles, excluding the sentinel (SharedData.lightTrianglesCount)
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
   uint32_t width;            // node width: 4 (BVH4; the only layout the kernels traverse)
-  uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack)
+  uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack; both trees)
+  // shadow-ray occluder tree (occluders.h): the BVH4 over the triangles that
+  // are not in a culled plane, stored after the main tree — its nodes are
+  // nodes [num_nodes, num_nodes + occ_nodes), its leaf triangles follow the
+  // num_triangles main ones.  occ_planes == 0: none (shadow rays traverse
+  // the main tree).  A shadow ray whose origin x has n.x - w <= -occ_margin
+  // for every culled plane (n, w) traverses it from occ_root (kEmptyChild:
+  // no triangle can occlude such a ray).
+  int32_t occ_root;
+  uint32_t occ_nodes;
+  uint32_t occ_tris;
+  uint32_t occ_planes;
+  float occ_margin;
+  float occ_plane[8][4];
 };
+constexpr uint32_t kMaxOccPlanes = 8;
 
 // camera-ray candidate lists (primary.h): header (offset << 8) | count per
 // 8x8 pixel block; count kPrimaryFallback = traverse the BVH

@@ -29,6 +29,7 @@
 #include "image.h"
 #include "kernels.h"
 #include "noise.h"
+#include "occluders.h"
 #include "primary.h"
 #include "scene.h"
 
@@ -49,6 +50,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 inline float bitsf(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+inline uint32_t fbits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 
 struct DevBuf {
   void* p = nullptr;
@@ -770,7 +772,58 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     o[11] = L.cdf;
     o[15] = bitsf(L.index);
   }
+  // shadow-ray occluder tree (occluders.h): a second BVH4 over the triangles
+  // outside the culled supporting planes, appended to the main tree's node
+  // and leaf-triangle arrays (refs rebased); host-SAH scenes only
+  std::vector<float> up_nodes = s->bvh.nodes, up_tris = s->bvh.tris;
+  mrt::OccluderSet occ;
+  mrt::BvhResult ob;
+  bool occ_on = builder == MRT_BVH_HOST_SAH && !desc->no_occluder_tree;
+  if (const char* v = std::getenv("MRT_OCCLUDERS")) occ_on = occ_on && std::atoi(v) != 0;
+  if (occ_on) {
+    std::vector<float> lv;
+    for (uint32_t l = 0; l < h.light_count; ++l)
+      for (const mrt::RefVertex* v : {&h.lights[l].v1, &h.lights[l].v2, &h.lights[l].v3})
+        lv.insert(lv.end(), {v->v[0], v->v[1], v->v[2]});
+    occ_on = mrt::find_occluders(h.vertices.data()->v, sizeof(mrt::RefVertex), (uint32_t)h.vertices.size(),
+                                 h.indices.data(), T, lv.data(), h.light_count, occ);
+  }
+  const uint32_t node_base = (uint32_t)(s->bvh.nodes.size() / 32), tri_base = T;
+  int32_t occ_root = mrt::kEmptyChild;
+  if (occ_on && !occ.keep.empty()) {
+    std::vector<uint32_t> sub;
+    sub.reserve(occ.keep.size() * 3);
+    for (uint32_t t : occ.keep) sub.insert(sub.end(), {h.indices[3 * t], h.indices[3 * t + 1], h.indices[3 * t + 2]});
+    mrt::BvhBuildOptions oo = opt;
+    oo.lds_node_budget = 0;
+    if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), sub.data(), (uint32_t)occ.keep.size(), oo, ob, err))
+      return fail(MRT_ERR_INVALID, "occluder BVH build failed: " + err);
+    auto rebase = [&](int32_t r) -> int32_t {
+      if (r == mrt::kEmptyChild) return r;
+      if (r >= 0) return r + (int32_t)node_base;
+      const uint32_t lr = ~(uint32_t)r;
+      return mrt::leaf_ref((lr >> mrt::kLeafCountBits) + tri_base, (lr & (mrt::kMaxLeafSize - 1)) + 1);
+    };
+    for (uint32_t k = 0; k < ob.num_nodes; ++k)
+      for (int c = 0; c < 4; ++c) {
+        float& f = ob.nodes[32 * (size_t)k + 24 + c];
+        f = bitsf((uint32_t)rebase((int32_t)fbits(f)));
+      }
+    for (size_t i = 0; i < occ.keep.size(); ++i) {   // leaf prim ids: subset position -> primitive
+      float& f = ob.tris[12 * i + 3];
+      f = bitsf(occ.keep[fbits(f)]);
+    }
+    occ_root = rebase(ob.root);
+    if (ob.num_nodes) up_nodes.insert(up_nodes.end(), ob.nodes.begin(), ob.nodes.begin() + 32 * (size_t)ob.num_nodes);
+    up_tris.insert(up_tris.end(), ob.tris.begin(), ob.tris.end());
+  }
   mrt_scene_info& in = s->info;
+  if (occ_on) {
+    in.occluder_planes = (uint32_t)occ.planes.size();
+    in.occluder_culled = occ.culled;
+    in.occluder_nodes = ob.num_nodes;
+    in.occluder_margin = occ.margin;
+  }
   in.vertices = (uint32_t)h.vertices.size();
   in.triangles = T;
   in.materials = (uint32_t)h.materials.size();
@@ -789,8 +842,8 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   }
   HIP_TRY(hipSetDevice(desc->device));
   if (builder == MRT_BVH_HOST_SAH) {
-    HIP_TRY(upload(s->nodes, s->bvh.nodes.data(), s->bvh.nodes.size() * 4));
-    HIP_TRY(upload(s->tris, s->bvh.tris.data(), s->bvh.tris.size() * 4));
+    HIP_TRY(upload(s->nodes, up_nodes.data(), up_nodes.size() * 4));
+    HIP_TRY(upload(s->tris, up_tris.data(), up_tris.size() * 4));
   }
   HIP_TRY(upload(s->prims, prims.data(), prims.size() * 4));
   HIP_TRY(upload(s->materials, mats.data(), mats.size() * 4));
@@ -809,6 +862,17 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.lds_nodes = s->bvh.lds_nodes;
   d.width = s->bvh.width;
   d.max_stack = s->bvh.max_stack;
+  d.occ_root = occ_root;
+  d.occ_planes = 0;
+  if (occ_on) {
+    d.occ_nodes = (uint32_t)(up_nodes.size() / 32) - s->bvh.num_nodes;   // (a leaf-root main tree keeps one dummy node)
+    d.occ_tris = (uint32_t)occ.keep.size();
+    d.occ_planes = (uint32_t)occ.planes.size();
+    d.occ_margin = occ.margin;
+    for (uint32_t k = 0; k < d.occ_planes; ++k)
+      for (int c = 0; c < 4; ++c) d.occ_plane[k][c] = occ.planes[k][c];
+    d.max_stack = std::max(d.max_stack, ob.max_stack);
+  }
   HIP_TRY(alloc_isect_spill(s->isect_spill, d.max_stack));
   in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
   *out = s.release();

@@ -63,6 +63,7 @@ class SceneDesc(ctypes.Structure):
         ("device", ctypes.c_int),
         ("bvh_width", ctypes.c_uint32),
         ("bvh_builder", ctypes.c_uint32),
+        ("no_occluder_tree", ctypes.c_uint32),
     ]
 
 
@@ -93,6 +94,8 @@ class SceneInfo(ctypes.Structure):
         ("bvh_depth", ctypes.c_uint32), ("bvh_lds_nodes", ctypes.c_uint32), ("bvh_width", ctypes.c_uint32),
         ("bvh_max_stack", ctypes.c_uint32), ("bvh_sah_cost", ctypes.c_double),
         ("build_ms", ctypes.c_double), ("device_bytes", ctypes.c_uint64),
+        ("occluder_planes", ctypes.c_uint32), ("occluder_culled", ctypes.c_uint32),
+        ("occluder_nodes", ctypes.c_uint32), ("occluder_margin", ctypes.c_float),
     ]
 
 
@@ -239,10 +242,11 @@ class Scene:
 
     def __init__(self, obj: str, mtl_override: str | None = None, *, procedural_triangles: int = 0,
                  procedural_seed: int = 1, max_leaf_size: int = 0, lds_nodes: int = 0, device: int = 0,
-                 bvh_width: int = 0, bvh_builder: int = 0):
+                 bvh_width: int = 0, bvh_builder: int = 0, occluder_tree: bool = True):
         self._h = None
         d = SceneDesc(scene_path(obj).encode(), (mtl_override or "").encode(), procedural_triangles,
-                      procedural_seed, max_leaf_size, lds_nodes, device, bvh_width, bvh_builder)
+                      procedural_seed, max_leaf_size, lds_nodes, device, bvh_width, bvh_builder,
+                      0 if occluder_tree else 1)
         h = ctypes.c_void_p()
         _check(lib().mrt_scene_create(ctypes.byref(d), ctypes.byref(h)), "mrt_scene_create")
         self._h = h

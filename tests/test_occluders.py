@@ -1,0 +1,171 @@
+"""CPU: the shadow-ray occluder tree (metal-renderer_amd/csrc/occluders.h).
+
+lightSamplingHandler (renderer/Shaders.metal:214-231) counts a light sample
+iff the shadow ray's nearest hit (renderer/Renderer.mm:545-553) is the target
+light triangle.  The product leaves the triangles of culled supporting planes
+(walls, floor, ceiling) out of a second BVH that shadow rays from origins
+inside those planes traverse.  These tests restate the plane choice and check
+the claim it rests on with the kernels' own float32 ray-triangle arithmetic
+(kernels.hip tri_bary, with and without FMA contraction): from an origin
+inside every culled plane by the margin, no culled triangle reports a hit in
+[0, t_light] — including origins at the margin and shadow rays grazing the
+ceiling the light hangs under.  (The GPU tests check the renders: precise
+build bit-identical to the oracle, which has no occluder tree, and fast
+build bitwise equal with the tree on and off.)
+"""
+import numpy as np
+import pytest
+
+from helpers import SEED
+
+
+def _supporting_planes(V, I, light_pts):
+    """Restatement of occluders.cpp's choice: planes of triangles with every
+    scene vertex on one side, every light vertex strictly inside."""
+    P = V[I.reshape(-1, 3)].astype(np.float64)
+    planes = []
+    culled = np.zeros(len(P), bool)
+    for t, (v0, v1, v2) in enumerate(P):
+        n = np.cross(v1 - v0, v2 - v0)
+        n /= np.linalg.norm(n)
+        w = n @ v0
+        s = V.astype(np.float64) @ n - w
+        tol = 1e-6
+        if (s > tol).any() and (s < -tol).any():
+            continue
+        if (s > tol).any():
+            n, w = -n, -w
+        if (light_pts @ n - w > -1e-4).any():
+            continue
+        culled[t] = True
+        if not any(np.allclose(n, q[:3]) and abs(w - q[3]) < 1e-6 for q in planes):
+            planes.append(np.array([*n, w]))
+    return np.array(planes), culled
+
+
+def _fma(a, b, c):
+    return (a.astype(np.float64) * b + c).astype(np.float32)
+
+
+def _tri_t(o, d, v0, e1, e2, fma):
+    """kernels.hip tri_bary in float32: (t, inside)."""
+    f32 = np.float32
+
+    def cross(a, b):
+        if fma:
+            return np.stack([_fma(a[..., 1], b[..., 2], -(a[..., 2] * b[..., 1])),
+                             _fma(a[..., 2], b[..., 0], -(a[..., 0] * b[..., 2])),
+                             _fma(a[..., 0], b[..., 1], -(a[..., 1] * b[..., 0]))], -1)
+        return np.stack([a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1],
+                         a[..., 2] * b[..., 0] - a[..., 0] * b[..., 2],
+                         a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]], -1)
+
+    def dot(a, b):
+        if fma:
+            return _fma(a[..., 2], b[..., 2], _fma(a[..., 1], b[..., 1], a[..., 0] * b[..., 0]))
+        return (a[..., 0] * b[..., 0] + a[..., 1] * b[..., 1]) + a[..., 2] * b[..., 2]
+
+    p = cross(d, e2)
+    det = dot(e1, p)
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        inv = f32(1.0) / det
+        s = o - v0
+        b1 = dot(s, p) * inv
+        q = cross(s, e1)
+        b2 = dot(d, q) * inv
+        t = dot(e2, q) * inv
+        ok = (det != 0) & (b1 >= 0) & (b1 <= 1) & (b2 >= 0) & (b1 + b2 <= 1)
+    return t, ok
+
+
+def test_occluder_planes_of_the_shipped_scenes(mrt_mod):
+    s = mrt_mod.Scene("cornellbox", device=-1)
+    assert s.info["occluder_planes"] == 5          # floor, ceiling, back, left, right walls
+    assert s.info["occluder_culled"] == 14         # their 10 triangles + the two boxes' bottoms
+    assert s.info["occluder_nodes"] >= 1
+    assert 0 < s.info["occluder_margin"] < 1e-4    # below DISTANCE_EPSILON: origins on the walls qualify
+    off = mrt_mod.Scene("cornellbox", device=-1, occluder_tree=False)
+    assert off.info["occluder_planes"] == 0 and off.info["occluder_culled"] == 0
+    # Water scenes: the walls are < 1/8 of 7 K triangles: no second tree
+    w = mrt_mod.Scene("CornellBox-Water-plastic", device=-1)
+    assert w.info["occluder_planes"] == 0
+
+
+@pytest.mark.parametrize("fma", [False, True])
+def test_culled_triangles_never_occlude(mrt_mod, fma):
+    s = mrt_mod.Scene("cornellbox", device=-1)
+    e = s.export()
+    V = e["vertices"]["v"]
+    I = e["indices"]
+    L = e["lights"][:-1]
+    light_pts = np.concatenate([L["v1"]["v"], L["v2"]["v"], L["v3"]["v"]]).astype(np.float64)
+    planes, culled = _supporting_planes(V, I, light_pts)
+    assert culled.sum() == s.info["occluder_culled"] and len(planes) == s.info["occluder_planes"]
+    margin = np.float32(s.info["occluder_margin"])
+
+    rng = np.random.default_rng(SEED)
+    n = 120_000
+    lo, hi = V.min(0), V.max(0)
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    # adversarial origins: at 1-2 margins from a random culled plane
+    k = n // 2
+    pl = planes[rng.integers(0, len(planes), k)]
+    dist = margin * rng.uniform(1.0, 2.0, k)
+    foot = o[:k] - ((o[:k].astype(np.float64) * pl[:, :3]).sum(1) - pl[:, 3])[:, None] * pl[:, :3]
+    o[:k] = (foot - dist[:, None] * pl[:, :3]).astype(np.float32)
+    # origins near the ceiling (shadow rays grazing the plane the light hangs under)
+    g = n // 8
+    o[k:k + g, 1] = np.float32(2.0) - margin * rng.uniform(1.0, 30.0, g).astype(np.float32)
+    # the kernel's selection: inside every culled plane by the margin (float32)
+    inside = np.ones(n, bool)
+    for p in planes.astype(np.float32):
+        inside &= (_fma(p[0], o[:, 0], _fma(p[1], o[:, 1], _fma(p[2], o[:, 2], -p[3]))) <= -margin)
+    o = o[inside]
+    assert len(o) > n // 2
+    # the light point and the shadow direction (as shade_hit: normalize(q - p))
+    li = rng.integers(0, len(L), len(o))
+    r1 = np.sqrt(rng.uniform(0, 1, len(o))).astype(np.float32)
+    r2 = rng.uniform(0, 1, len(o)).astype(np.float32)
+    bu, bv, bw = 1 - r1, r1 * (1 - r2), r1 * r2
+    q = (L["v1"]["v"][li] * bu[:, None] + L["v2"]["v"][li] * bv[:, None] + L["v3"]["v"][li] * bw[:, None])
+    q = q.astype(np.float32)
+    d = q - o
+    d = (d / np.sqrt((d * d).sum(1, keepdims=True))).astype(np.float32)
+    # t of the target light triangle
+    tgt = L["index"][li]
+    Pv = V[I.reshape(-1, 3)]
+    tv0 = Pv[tgt, 0]
+    tT, ok = _tri_t(o, d, tv0, Pv[tgt, 1] - tv0, Pv[tgt, 2] - tv0, fma)
+    o, d, tT = o[ok], d[ok], tT[ok]
+    assert len(o) > n // 3
+    for t in np.nonzero(culled)[0]:
+        v0 = Pv[t, 0]
+        tt, hit = _tri_t(o, d, v0[None], (Pv[t, 1] - v0)[None], (Pv[t, 2] - v0)[None], fma)
+        bad = hit & (tt >= 0) & (tt <= tT)
+        assert not bad.any(), (t, o[bad][:3], d[bad][:3], tt[bad][:3], tT[bad][:3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["stream", "bounce", "path"])
+@pytest.mark.parametrize("precise", [True, False])
+@pytest.mark.parametrize("scene,W,H,L", [("cornellbox", 96, 64, 4), ("white-box", 80, 48, 5),
+                                         ("cornellbox", 130, 70, 8)])
+def test_gpu_occluder_tree_renders_bitwise(gpu, mrt_mod, monkeypatch, kernel, precise, scene, W, H, L):
+    """Shadow rays through the occluder tree give the same answers as through
+    the whole scene: images and ray counts bitwise equal with the tree on and
+    off, in every kernel (stream, per-bounce, path) and both builds."""
+    monkeypatch.setenv("MRT_STREAM", "0" if kernel == "bounce" else "1")
+    if kernel == "path":
+        monkeypatch.setenv("MRT_KERNEL", "path")
+    out = []
+    for tree in (True, False):
+        s = mrt_mod.Scene(scene, occluder_tree=tree)
+        assert (s.info["occluder_planes"] > 0) == tree
+        r = mrt_mod.Renderer(s, W, H, L, precise=precise)
+        r.draw(3)
+        out.append((r.read_image(), r.stats()["active_ray_bounces"]))
+        r.close()
+        s.close()
+    (a, na), (b, nb) = out
+    assert np.isfinite(a).all() and a[..., :3].max() > 0
+    assert a.tobytes() == b.tobytes() and na == nb
