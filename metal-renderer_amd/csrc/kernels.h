@@ -143,6 +143,8 @@ constexpr uint32_t kShadeDebugMaterial = 1u;   // BounceArgs::flags / launch_sha
   hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries,           \
                            uint32_t grid, hipStream_t s);                                                 \
   bool stream_supported(const DeviceScene& sc, uint32_t stack_entries);                                   \
+  /* the stream kernel's persistent grid (its LDS has no per-block segment scratch) */                    \
+  hipError_t stream_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                  \
   /* the scene's LDS staging mode is not "whole scene in LDS": the path kernel is the faster one */      \
   bool path_preferred(const DeviceScene& sc);                                                             \
   /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \

@@ -2098,6 +2098,24 @@ hipError_t launch_stream_t(const DeviceScene& sc, const BounceArgs& a, uint32_t 
   stream_kernel<STACK, kAllLds><<<dim3(grid), dim3(kBlock), bounce_lds_bytes(sc, kAllLds, STACK, 0), s>>>(sc, a);
   return hipGetLastError();
 }
+// the stream kernel's own persistent grid: every block slot its LDS (scene
+// image + stack, no segment scratch) and registers leave on a CU
+template <int STACK>
+hipError_t stream_grid_t(const DeviceScene& sc, uint32_t* grid) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return e;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, stream_kernel<STACK, kAllLds>, kBlock,
+                                                   bounce_lds_bytes(sc, kAllLds, STACK, 0)) != hipSuccess || occ < 1)
+    occ = 1;
+  *grid = (uint32_t)prop.multiProcessorCount * (uint32_t)std::min(occ, 8);
+  return hipSuccess;
+}
+
 bool stream_ok(const DeviceScene& sc, uint32_t stack_entries) {
   return sc.width == 4 && choose_mode(sc) == kAllLds && sc.max_stack <= stack_entries && stack_entries <= 32;
 }
@@ -2294,6 +2312,15 @@ hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* gr
 bool path_preferred(const DeviceScene& sc) { return choose_mode(sc) != kAllLds; }
 
 bool stream_supported(const DeviceScene& sc, uint32_t stack_entries) { return stream_ok(sc, stack_entries); }
+
+hipError_t stream_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid) {
+  if (!stream_ok(sc, stack_entries)) return hipErrorNotSupported;
+  if (stack_entries <= 8) return stream_grid_t<8>(sc, grid);
+  if (stack_entries <= 12) return stream_grid_t<12>(sc, grid);
+  if (stack_entries <= 16) return stream_grid_t<16>(sc, grid);
+  if (stack_entries <= 24) return stream_grid_t<24>(sc, grid);
+  return stream_grid_t<32>(sc, grid);
+}
 
 hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,
                          hipStream_t s) {

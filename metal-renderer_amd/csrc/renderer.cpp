@@ -1228,13 +1228,6 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     r->primary_cap = std::max<uint32_t>(1, std::min<uint32_t>(mrt::kPrimaryFallback - 1, (uint32_t)std::strtoul(v, nullptr, 0)));
   r->path_mode = mrt::fast::path_preferred(desc->scene->dev);
   if (const char* k = std::getenv("MRT_KERNEL")) r->path_mode = std::strcmp(k, "path") == 0;
-  if (r->path_mode)
-    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::path_grid(r->scene->dev, r->stack_entries, &r->grid)
-                                             : mrt::fast::path_grid(r->scene->dev, r->stack_entries, &r->grid));
-  else
-    HIP_TRY((desc->flags & MRT_FLAG_PRECISE) ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid)
-                                             : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid));
-  if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
   // streaming wavefront (one launch per frame batch, per-wave ray queues)
   // for whole-scene-in-LDS scenes; MRT_STREAM=0 keeps one launch per bounce
   {
@@ -1243,6 +1236,21 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
     r->stream_allowed = want && !r->path_mode && desc->max_path_length <= mrt::kStreamMaxL &&
                         mrt::fast::stream_supported(desc->scene->dev, r->stack_entries);
   }
+  // persistent grid of the kernel this renderer launches: the stream kernel
+  // sizes it by its own LDS (the per-bounce kernel's segment scratch grows
+  // with the grid: sized for that, a 24-KB scene image + stack left C2 at 4
+  // instead of 5 blocks per CU)
+  const bool precise = (desc->flags & MRT_FLAG_PRECISE) != 0;
+  if (r->path_mode)
+    HIP_TRY(precise ? mrt::precise::path_grid(r->scene->dev, r->stack_entries, &r->grid)
+                    : mrt::fast::path_grid(r->scene->dev, r->stack_entries, &r->grid));
+  else if (r->stream_allowed)
+    HIP_TRY(precise ? mrt::precise::stream_grid(r->scene->dev, r->stack_entries, &r->grid)
+                    : mrt::fast::stream_grid(r->scene->dev, r->stack_entries, &r->grid));
+  else
+    HIP_TRY(precise ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid)
+                    : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid));
+  if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
   int rc = alloc_frame_buffers(r.get());
   if (rc) return rc;
   *out = r.release();
