@@ -180,11 +180,12 @@ def test_pipelined_tile_share_bitwise(gpu, mrt_mod, monkeypatch, scene, L):
         assert x.tobytes() == y.tobytes()
 
 
-def test_device_spans_match_events(gpu, mrt_mod):
+def test_device_spans_match_events(gpu, mrt_mod, monkeypatch):
     """Every frame batch's render launch records its device span (earliest
     block start to latest wave end, the chip's wall clock); with one render
     stream the HIP events around the launch bracket the same span, so the
     two timings agree (events include the launch latency: >= span)."""
+    monkeypatch.setenv("MRT_INFLIGHT", "1")   # the default is two render streams
     sc = mrt_mod.Scene("cornellbox")
     r = mrt_mod.Renderer(sc, 960, 540, 4, profile=True)
     r.draw(16)
