@@ -5,6 +5,11 @@
 # (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).
 TAG=${1:-r1}; CFG=${2:-c2}; shift 2
 export TMPDIR=/tmp
+# one render stream: the renderer's default two frame batches in flight
+# overlap consecutive launches, which stretches each launch's trace span
+# (the bench times them by device spans instead); counters per launch are
+# the same either way
+export MRT_INFLIGHT=${MRT_INFLIGHT:-1}
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
 # the library these passes measure (bench.py compares it with the one it loads)
