@@ -9,7 +9,7 @@ run() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs pyt
 run c1 300 --config c1 --steps 5 --warmup 1
 run c2 400 --config c2 --steps 5 --warmup 1
 run c2s8 200 --config c2 --steps 40 --warmup 5 --shard-of 8 --no-cpu-baseline
-run c2L5 200 --config c2 --steps 3 --warmup 1 --max-path-length 5 --no-cpu-baseline
+run c2L5 200 --config c2 --steps 20 --warmup 3 --max-path-length 5 --no-cpu-baseline
 run c3 400 --config c3 --steps 2 --warmup 1
 run c3g 400 --config c3g --steps 2 --warmup 1
 run c4 400 --config c4 --steps 3 --warmup 1
