@@ -509,7 +509,14 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
       t[i] = ti_;                                         \
       r[i] = ri_;                                         \
     }
-    MRT_CE(0, 1) MRT_CE(2, 3) MRT_CE(0, 2) MRT_CE(1, 3) MRT_CE(1, 2)
+    if (!(ANY && MODE == kAllLds)) {
+      MRT_CE(0, 1) MRT_CE(2, 3) MRT_CE(0, 2) MRT_CE(1, 3) MRT_CE(1, 2)
+    } else {
+      // occlusion in an all-in-LDS tree: only the nearest hit child is
+      // picked, the others are pushed in slot order (C2 +0.5 %: 9661 / 9646
+      // vs 9587 / 9613; global-memory trees keep the full sort, C4 =)
+      MRT_CE(0, 1) MRT_CE(0, 2) MRT_CE(0, 3)
+    }
 #undef MRT_CE
 #if MRT_PUSH3
     if (MODE != kAllLds) {
