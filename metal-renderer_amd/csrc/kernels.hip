@@ -496,7 +496,7 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
       r[0] = (int32_t)fbits(q[6].x); r[1] = (int32_t)fbits(q[6].y); r[2] = (int32_t)fbits(q[6].z); r[3] = (int32_t)fbits(q[6].w);
     }
     const float inf = __builtin_inff();
-    // near-to-far order for occlusion rays too: measured +2.5 % (C2) and
+    // near-to-far order for occlusion rays too: measured +2.5 % (C2, r1) and
     // +4.5 % (C4) over slot order — near children hold the likely occluders
     // 4-input sorting network on (t, ref); misses (+inf) sink to the end
 #define MRT_CE(i, j)                                      \
@@ -509,12 +509,15 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
       t[i] = ti_;                                         \
       r[i] = ri_;                                         \
     }
-    if (!(ANY && MODE == kAllLds)) {
+    if (MODE != kAllLds) {
       MRT_CE(0, 1) MRT_CE(2, 3) MRT_CE(0, 2) MRT_CE(1, 3) MRT_CE(1, 2)
     } else {
-      // occlusion in an all-in-LDS tree: only the nearest hit child is
-      // picked, the others are pushed in slot order (C2 +0.5 %: 9661 / 9646
-      // vs 9587 / 9613; global-memory trees keep the full sort, C4 =)
+      // all-in-LDS trees: only the nearest hit child is picked, the others
+      // are pushed in slot order — the full sort's 10 more VALU ops per node
+      // cost more than the better pop order saves in a shallow tree (C2:
+      // occlusion queries +0.5 %, 9661 / 9646 vs 9587 / 9613; nearest
+      // queries too, another +2.8 %, 9895 / 9898 vs 9630 / 9635).
+      // Global-memory trees keep the full sort (C4 = for occlusion).
       MRT_CE(0, 1) MRT_CE(0, 2) MRT_CE(0, 3)
     }
 #undef MRT_CE
