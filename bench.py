@@ -489,8 +489,13 @@ def main():
     avg_launch_ms = kms / max(1, timed)
     launch_timing = "hip-events on the render stream"
     if st["inflight"] > 1 and spans and spans == launches:
-        avg_launch_ms, timed = avg_span_ms, spans
-        launch_timing = "device spans (launches on 2 streams overlap)"
+        # a launch queued behind the previous one starts a few blocks early
+        # and the rest once CUs free up, so its span can exceed its share of
+        # the step: never more than the step's time per launch
+        per_launch_ms = ms_per_step * args.steps / max(1, launches)
+        avg_launch_ms, timed = min(avg_span_ms, per_launch_ms), spans
+        launch_timing = ("device spans (launches on 2 streams overlap)" if avg_span_ms <= per_launch_ms
+                         else "step time per launch (device spans of overlapped launches exceed it)")
     launch_s = avg_launch_ms * 1e-3
     launches_per_step = launches / max(1, args.steps)
     roof = roofline(args, pmc_path=args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json"),
