@@ -59,6 +59,11 @@ CONFIGS = {
     # configs[3]: 1M-triangle procedural mesh in the cornellbox shell, 64 spp, L = 4
     "c4": dict(workload="C4 1M-triangle procedural mesh 1920x1080 64spp L=4", scene="cornellbox", mtl=None,
                width=1920, height=1080, spp=64, L=4, procedural=1 << 20),
+    # C2 at MAX_PATH_LENGTH 5: north_star's "primary ray + 4 bounces" reading
+    # of the headline (C2's L = 4 is the primary ray + 3 bounces as
+    # renderer/Renderer.mm:517 loops MAX_PATH_LENGTH, Raytracing.h:23)
+    "c2l5": dict(workload="C2 at L=5: cornellbox 1920x1080 64spp, primary ray + 4 bounces (diffuse BSDF)",
+                 scene="cornellbox", mtl=None, width=1920, height=1080, spp=64, L=5, procedural=0),
     # configs[4]: C4's scene at 4K, 256 spp, L = 8 — the 8-GPU configuration
     # (one GPU's share is measured with --shard-of 8)
     "c5": dict(workload="C5 1M-triangle procedural mesh 3840x2160 256spp L=8", scene="cornellbox", mtl=None,
@@ -198,14 +203,21 @@ def lib_md5(path):
     return h.hexdigest()
 
 
-def host_threads():
-    """The CPUs this process may run on: the affinity mask, capped by the
-    worker-pool size the GPU box sets for one GPU's share (OMP_NUM_THREADS=16
-    there; os.cpu_count() reports the whole 256-CPU machine)."""
+def affinity_cpus():
     try:
-        n = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
+        return os.cpu_count() or 1
+
+
+def host_threads():
+    """Worker threads of the CPU baseline: the CPUs this process may run on
+    (affinity mask), capped by the worker-pool size the GPU pool sets for one
+    GPU's share of a shared 8-GPU host (OMP_NUM_THREADS=16 there, with the
+    rule to size worker pools to that share; the affinity mask and
+    os.cpu_count() report the whole 256-CPU machine).  Without the variable
+    (e.g. a dedicated host) every CPU of the affinity mask is used."""
+    n = affinity_cpus()
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return max(1, min(n, cap) if cap > 0 else n)
 
@@ -272,6 +284,10 @@ def cpu_baseline(cfg, frames):
     dt1 = time.perf_counter() - t1
     base = {"value": round(paths / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
             "single_thread_value": round(W * rows1 * f1 / dt1 / 1e6, 4), "host_cpus": os.cpu_count(),
+            "affinity_cpus": affinity_cpus(),
+            "cores_policy": ("threads = the affinity mask capped by OMP_NUM_THREADS, the worker-pool size the GPU "
+                             "pool sets for one GPU's CPU share of the shared host (its rule: size worker pools to "
+                             "that share); the whole affinity mask is not used there"),
             "cpu_model": _cpu_model(),
             "sample": f"frames 0-{frames - 1}, rows {y0}-{y0 + rows - 1} of the workload ({W}x{rows} of {W}x{H}, "
                       f"L={cfg['L']}, {paths} paths), nearest hits through a binned-SAH BVH over "
@@ -316,9 +332,15 @@ def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_
       valu — SQ_INSTS_VALU x 64 lane-slots per launch / launch time, against
              1024 SIMDs x 32 lanes/cycle x 2.4 GHz (a wave64 VALU instruction
              holds its SIMD's issue for 2 cycles whatever its exec mask).
-    bound = the roof with the larger fraction (the counter-measured limiter);
-    *_vs_step = the same counts per step over ms_per_step (<= frac: the check
-    against the wall clock)."""
+    bound = the roof with the larger fraction (the counter-measured limiter).
+    Three clocks for the same per-launch counts: `frac` (the headline) divides
+    by the wall-clock step time per launch (ms_per_step x steps / launches:
+    includes the accumulate pass and launch gaps, never favourable);
+    `frac_vs_launch` by this run's per-launch kernel time (HIP events, or the
+    device span with launches on two streams); `frac_vs_profile` by the
+    rocprofv3 trace's average duration of the same kernel (profiles/, one
+    render stream).  valu_useful_* = the VALU fraction x valu_lane_util: the
+    share of the issue roof doing work in active lanes."""
     import mrt
     out = {"bound": "unmeasured", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
     if not (os.path.exists(pmc_path) and not args.precise and (args.pmc or whole_frame) and timed):
@@ -329,31 +351,49 @@ def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_
         pmc = json.load(f)
     traffic = pmc.get("hbm_bytes_per_launch")
     valu_insts = (pmc.get("sq") or {}).get("SQ_INSTS_VALU")
+    lane_util = pmc.get("valu_lane_util")
+    step_launch_s = step_s / max(1e-9, launches_per_step)     # wall-clock step time per launch
+    prof_s = (pmc.get("avg_launch_ns_rocprof_timed") or pmc.get("avg_launch_ns_rocprof") or 0) * 1e-9
     roofs = {}
+
+    def fracs(per_launch, peak):
+        f = {"frac": round(per_launch / step_launch_s / peak, 4),
+             "frac_vs_launch": round(per_launch / launch_s / peak, 4)}
+        if prof_s:
+            f["frac_vs_profile"] = round(per_launch / prof_s / peak, 4)
+        return f
+
     if traffic:
-        gbs = traffic / launch_s / 1e9
+        gbs = traffic / step_launch_s / 1e9
         roofs["hbm"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBS, 4),
-                        "frac_vs_step": round(traffic * launches_per_step / step_s / 1e9 / HBM_PEAK_GBS, 4),
-                        "bytes_per_launch": traffic}
+                        **fracs(traffic / 1e9, HBM_PEAK_GBS), "bytes_per_launch": traffic}
     if valu_insts:
-        t = valu_insts * 64 / launch_s / 1e12
-        roofs["valu-issue"] = {"achieved": round(t, 2), "peak": round(VALU_PEAK_TLANE, 2),
-                               "unit": "T VALU lane-slots/s", "frac": round(t / VALU_PEAK_TLANE, 4),
-                               "frac_vs_step": round(valu_insts * 64 * launches_per_step / step_s / 1e12
-                                                     / VALU_PEAK_TLANE, 4),
-                               "wave_instructions_per_launch": valu_insts}
+        t = valu_insts * 64 / step_launch_s / 1e12
+        v = {"achieved": round(t, 2), "peak": round(VALU_PEAK_TLANE, 2), "unit": "T VALU lane-slots/s",
+             **fracs(valu_insts * 64 / 1e12, VALU_PEAK_TLANE), "wave_instructions_per_launch": valu_insts}
+        if lane_util:
+            for k in ("frac", "frac_vs_launch", "frac_vs_profile"):
+                if k in v:
+                    v["valu_useful_" + k] = round(v[k] * lane_util, 4)
+        roofs["valu-issue"] = v
     if not roofs:
         out["note"] = f"{os.path.basename(pmc_path)} holds no counts"
         return out
     bound = max(roofs, key=lambda k: roofs[k]["frac"])
-    out.update({k: roofs[bound][k] for k in ("achieved", "peak", "unit", "frac", "frac_vs_step")})
+    out.update({k: roofs[bound].get(k) for k in ("achieved", "peak", "unit", "frac", "frac_vs_launch",
+                                                  "frac_vs_profile")})
+    if "valu-issue" in roofs:
+        out["valu_useful_frac"] = roofs["valu-issue"].get("valu_useful_frac")
     out.update({"bound": bound, "traffic": traffic, "roofs": roofs,
+                "clocks": {"frac": f"wall-clock step time per launch {step_launch_s * 1e3:.4f} ms",
+                           "frac_vs_launch": f"this run's per-launch kernel time {launch_s * 1e3:.4f} ms",
+                           "frac_vs_profile": (f"rocprofv3 trace average {prof_s * 1e3:.4f} ms"
+                                               if prof_s else None)},
                 "wait_any_frac": pmc.get("wait_any_frac"),
-                "valu_lane_util": pmc.get("valu_lane_util"),
+                "valu_lane_util": lane_util,
                 "pmc_clock_ghz": pmc.get("clock_ghz"),
-                "rocprof_avg_launch_ms": round(pmc["avg_launch_ns_rocprof"] / 1e6, 4)
-                if pmc.get("avg_launch_ns_rocprof") else None,
+                "rocprof_avg_launch_ms": round(prof_s * 1e3, 4) if prof_s else None,
+                "rocprof_timed_launches": pmc.get("timed_launches_rocprof"),
                 "source": f"profiles/{os.path.basename(pmc_path)} (tag {pmc.get('tag')}, commit "
                           f"{pmc.get('commit', 'unrecorded')}, lib md5 {pmc.get('lib_md5')})",
                 "same_library": (pmc.get("lib_md5") == lib_md5(mrt.LIB_PATH)) if pmc.get("lib_md5") else None})
@@ -398,6 +438,7 @@ def main():
     r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=not args.no_kernel_timing,
                      shard_rank=(args.shard_rank if args.shard_of else rank), shard_count=shard_count)
     r.prepare(spp)
+    prep = r.stats()   # noise window of the step's spp frames, generated + uploaded before the timed region
 
     # multi-GPU exchange: every rank's owned 64x64 tiles go
     # to rank 0 through libmrt's RCCL communicator (include/mrt.h
@@ -520,6 +561,25 @@ def main():
         "alg_bytes_per_launch": int(bytes_alg / max(1, launches)),
         "active_ray_bounces_per_step": int(A / max(1, args.steps))})
 
+    # the noise schedule's host cost: the reference regenerates
+    # one 64x64 float4 table per frame on one CPU thread before the frame's
+    # commit (renderer/Renderer.mm:486-496); libmrt generates the step's
+    # window ahead of the timed region (mrt_renderer_prepare, host threads +
+    # one upload).  Both per frame: a progressive render past the window pays
+    # the latter inside draw.
+    mrt.noise_table(mrt.DEFAULT_SEED, 0)   # first call imports numpy
+    t_n = time.perf_counter()
+    for f in range(32):
+        mrt.noise_table(mrt.DEFAULT_SEED, f)
+    noise_1t_ms = (time.perf_counter() - t_n) * 1e3 / 32
+    noise = {"noise_ms_per_frame": round(noise_1t_ms, 4),
+             "noise_ms_per_frame_note": "one table generated on one host thread (mrt_noise_table), the "
+                                        "reference's per-frame CPU cost model; not in the timed steps",
+             "prepare_ms_per_frame": round(prep["noise_ms"] / max(1, prep["noise_tables"]), 4),
+             "prepare_tables": int(prep["noise_tables"]),
+             "prepare_note": "mrt_renderer_prepare: the window's tables on the library's host threads + one "
+                             "upload, per table"}
+
     result = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -548,6 +608,8 @@ def main():
                            "max_stack": scene.info["bvh_max_stack"]}},
         "roofline": roof,
         "cpu_baseline": None,
+        "noise_ms_per_frame": noise["noise_ms_per_frame"],
+        "noise": noise,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:
         base_cpu, ref_img, mask, frames = cpu_baseline(cfg, args.cpu_frames or spp)

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 6
+#define MRT_ABI_VERSION 7
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -108,6 +108,9 @@ typedef struct mrt_scene_info {
    * other triangles (same answers).  0 planes = no occluder tree. */
   uint32_t occluder_planes, occluder_culled, occluder_nodes;
   float occluder_margin;
+  uint32_t occluder_max_stack;     /* traversal stack entries the occluder tree can need (<= bvh_max_stack:
+                                      a deeper occluder tree is not built); renderers size their stack by
+                                      the deeper tree.  ABI 7. */
 } mrt_scene_info;
 
 int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out);
@@ -208,6 +211,12 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
   uint32_t primary_blocks;         /* 8x8 pixel blocks whose camera rays test a candidate list instead of
                                       traversing the BVH (0 = lists off; MRT_PRIMARY=0 disables) */
   float primary_mean;              /* mean candidate-list length over those blocks */
+  /* ABI 7: host cost of the noise schedule (the reference regenerates one
+   * table per frame on the CPU before the frame's commit, Renderer.mm:486-496;
+   * here mrt_renderer_prepare / draw_n generate a window of tables on the host
+   * threads and upload it once) */
+  double noise_ms;                 /* host wall time generating + uploading noise tables */
+  uint64_t noise_tables;           /* per-frame tables generated (noise_ms / noise_tables = cost per frame) */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);
@@ -363,6 +372,19 @@ int mrt_debug_stamps(uint64_t* out8, int reset);
  * grab latency, last grab's latency, phase cycles 0..4} in 100 MHz real-time ticks; n = number
  * of uint64 to copy (at most 4 * 8192 * 16).  Zeros outside the stamp library. */
 int mrt_debug_wave_times(uint64_t* out, size_t n);
+/* Diagnostics (ABI 7): lane-occupancy counters of the separately built
+ * lane-statistics library (make variant VNAME=lanes VFLAGS=-DMRT_LANESTATS=1):
+ * out[k] for k < n (at most 64), summed over every wave of every launch since
+ * the last reset — per traversal loop the wave iterations and the active
+ * lanes in them (tools/lane_stats.py names the slots).  Zeros otherwise. */
+int mrt_debug_lanes(uint64_t* out, size_t n, int reset);
+/* Test entry (ABI 7): rank 0's unpack of an N-rank gather without a
+ * communicator.  `gathered` (host) holds nranks slabs of
+ * mrt_tiles_packed_floats(W, H, 0, nranks) floats, rank k's at slab k, as the
+ * gather of MRT_EXCHANGE_GATHER delivers them; the renderer (shard_rank 0,
+ * shard_count nranks) unpacks slabs 1..N-1 into its image with the RCCL
+ * path's own unpack.  Synchronises the renderer. */
+int mrt_debug_exchange_unpack(mrt_renderer* r, uint32_t nranks, const float* gathered, size_t floats);
 /* Number of HIP devices visible (0 when none; never fails). */
 int mrt_device_count(void);
 

@@ -160,6 +160,8 @@ constexpr uint32_t kShadeDebugMaterial = 1u;   // BounceArgs::flags / launch_sha
   hipError_t read_stamps(unsigned long long* out8, bool reset);                                          \
   /* per-wave timeline {start, exit, iterations} of the last launch of each bounce % 4 (stamp builds) */   \
   hipError_t read_wave_times(unsigned long long* out, size_t n);                                         \
+  /* diagnostic lane statistics (MRT_LANESTATS builds; zeros otherwise) */                                 \
+  hipError_t read_lane_stats(unsigned long long* out, size_t n, bool reset);                             \
   }
 
 MRT_DECLARE_LAUNCHERS(precise)

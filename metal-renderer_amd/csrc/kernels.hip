@@ -326,19 +326,6 @@ __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx&
 #pragma unroll
       for (int i = 0; i < 6; ++i) q[i] = p[row[i]];
       q[6] = p[6];
-#ifdef EXP_DOUBLE_LOADS
-      {
-        uint32_t d0, d1, d2, d3, d4, d5, d6;
-        asm volatile("global_load_dword %0, %1, off offset:0" : "=v"(d0) : "v"(p));
-        asm volatile("global_load_dword %0, %1, off offset:16" : "=v"(d1) : "v"(p));
-        asm volatile("global_load_dword %0, %1, off offset:32" : "=v"(d2) : "v"(p));
-        asm volatile("global_load_dword %0, %1, off offset:48" : "=v"(d3) : "v"(p));
-        asm volatile("global_load_dword %0, %1, off offset:64" : "=v"(d4) : "v"(p));
-        asm volatile("global_load_dword %0, %1, off offset:80" : "=v"(d5) : "v"(p));
-        asm volatile("global_load_dword %0, %1, off offset:96" : "=v"(d6) : "v"(p));
-        asm volatile("s_waitcnt vmcnt(0)" : : "v"(d0), "v"(d1), "v"(d2), "v"(d3), "v"(d4), "v"(d5), "v"(d6));
-      }
-#endif
     }
   }
 }
@@ -444,6 +431,44 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   return cx;
 }
 
+// ---------------------------------------------------------------------------
+// Diagnostic lane statistics (MRT_LANESTATS builds only; never the product):
+// per wave, for each traversal loop, the loop iterations and the active lanes
+// in them (lane utilisation of that loop = lanes / (64 x iterations)), and the
+// lanes entering each phase.  Kept per wave in LDS by the wave's first active
+// lane, summed into g_lanes at the wave's exit.  Slots (tools/lane_stats.py):
+//   0-5   nearest query: lanes, wave calls, interior iterations, interior
+//         lane-steps, leaf iterations, leaf lane-steps
+//   6-11  the same for occlusion queries
+//   12-13 shading: wave calls, lanes;  14-15 bounce_wave: calls, active lanes
+//   16-17 shadow phase: lanes with a shadow ray, wave calls with any
+//   18-19 camera-ray candidate lists: wave calls, lanes
+//   20-25 path kernel: service rounds, lanes serviced, traversal rounds,
+//         lanes traversing in them, lanes refilled, outer iterations
+//   26-27 stream kernel: camera iterations, queue-level iterations
+// ---------------------------------------------------------------------------
+#ifndef MRT_LANESTATS
+#define MRT_LANESTATS 0
+#endif
+#if MRT_LANESTATS
+constexpr int kLaneStats = 32;
+__shared__ unsigned long long s_lanes[kBlock / 64][kLaneStats];
+__device__ unsigned long long g_lanes[kLaneStats];
+__device__ __forceinline__ void ls_add(int k, uint32_t v) {
+  const uint64_t m = __ballot(1);
+  if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((unsigned long long)m) - 1)) s_lanes[threadIdx.x >> 6][k] += v;
+}
+__device__ __forceinline__ uint32_t ls_lanes() { return (uint32_t)__popcll(__ballot(1)); }
+#define LS_ADD(k, v) ls_add((k), (v))
+#define LS_INIT() do { if ((threadIdx.x & 63u) < (uint32_t)kLaneStats) s_lanes[threadIdx.x >> 6][threadIdx.x & 63u] = 0; } while (0)
+#define LS_FLUSH() do { const uint32_t l_ = threadIdx.x & 63u; \
+    if (l_ < (uint32_t)kLaneStats && s_lanes[threadIdx.x >> 6][l_]) atomicAdd(&g_lanes[l_], s_lanes[threadIdx.x >> 6][l_]); } while (0)
+#else
+#define LS_ADD(k, v) do {} while (0)
+#define LS_INIT() do {} while (0)
+#define LS_FLUSH() do {} while (0)
+#endif
+
 // While-while traversal with postponed leaves (Aila & Laine 2009, recast for
 // 64-lane waves): a lane that reaches a leaf parks it and keeps descending
 // interior nodes until every lane of the wave holds a leaf, then the wave
@@ -466,6 +491,9 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 // trees lose by it (C2, the stream kernel: slack 2 -1.3 %, 8 -3.4 %).
 #ifndef MRT_TRAV_SLACK   // traverse(): stream / bounce / stage kernels
 #define MRT_TRAV_SLACK 0
+#endif
+#ifndef MRT_TRAV_LEAF_SLACK   // traverse()'s leaf loop: a lane keeps its untested leaf for the next round
+#define MRT_TRAV_LEAF_SLACK 0
 #endif
 #ifndef MRT_PATH_SLACK   // trav_round(): the path kernel
 #define MRT_PATH_SLACK 12
@@ -637,10 +665,16 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
   const RayBox rb = make_raybox(o, d);
   int32_t node = root, leaf = 0;
   int sp = 0;
+  constexpr int kLs = ANY ? 6 : 0;
+  (void)kLs;
+  LS_ADD(kLs + 0, ls_lanes());
+  LS_ADD(kLs + 1, 1);
   if (node < 0) { leaf = node; node = kDone; }
   while (node != kDone || leaf != 0) {
     // interior nodes
     while (node != kDone && node >= 0) {
+      LS_ADD(kLs + 2, 1);
+      LS_ADD(kLs + 3, ls_lanes());
       node = interior_step<STACK, MODE, ANY>(sc, cx, node, o, rb, tmin, h.t, sp);
       if (node < 0 && leaf == 0) {   // park the leaf, keep descending
         leaf = node;
@@ -650,6 +684,8 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
     }
     // leaves
     while (leaf < 0) {
+      LS_ADD(kLs + 4, 1);
+      LS_ADD(kLs + 5, ls_lanes());
       const uint32_t lr = ~(uint32_t)leaf;
       const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
       if (leaf_tests<MODE>(sc, cx, o, d, tmin, first, cnt, h, ANY, target, nullptr)) return true;
@@ -658,6 +694,9 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
         leaf = node;
         node = stack_pop<STACK>(cx, sp);
       }
+#if MRT_TRAV_LEAF_SLACK > 0
+      if ((uint32_t)__popcll(__ballot(leaf < 0)) <= (uint32_t)MRT_TRAV_LEAF_SLACK) break;
+#endif
     }
   }
   return false;
@@ -699,16 +738,48 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
   return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, shadow_root(sc, o));
 }
 
+// The shadow ray's own surface first (exact early-out, r4).  The occlusion
+// query answers "occluded" as soon as ANY primitive k != target passes the
+// leaf test with (t_k, k) < (t_T, target) in [0, t_T]; the triangle the ray
+// leaves is such a k whenever the light lies behind that triangle's plane
+// (the ray re-crosses the surface ~1e-4 from its origin: about half of a
+// closed mesh's shadow rays, each of which would otherwise descend the tree
+// to the origin's own leaf).  It is tested with the leaf test's arithmetic
+// (tri_bary over the shading record's vertices: the leaf record's v0,
+// e1 = v1 - v0, e2 = v2 - v0 are the same float operations, bvh.cpp) and its
+// acceptance rule, so "occluded" here is the traversal's answer and
+// "not occluded" changes nothing (MRT_ORIGIN_TEST=0 turns it off).
+#ifndef MRT_ORIGIN_TEST
+#define MRT_ORIGIN_TEST 1
+#endif
+template <int MODE>
+__device__ __forceinline__ bool origin_occludes(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t prim,
+                                                uint32_t target, float tT) {
+#if MRT_ORIGIN_TEST
+  const V3 p0 = mk(fetch_prim<MODE>(sc, cx, prim, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, prim, 1));
+  const V3 p2 = mk(fetch_prim<MODE>(sc, cx, prim, 2));
+  float t, u, v;
+  const bool ok = tri_bary(o, d, p0, sub(p1, p0), sub(p2, p0), t, u, v);
+  return ok & (prim != target) & (t >= 0.0f) & (t <= tT) & ((t < tT) | (prim < target));
+#else
+  (void)sc; (void)cx; (void)o; (void)d; (void)prim; (void)target; (void)tT;
+  return false;
+#endif
+}
+
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
 // (renderer/Shaders.metal:214-231): contributes iff the nearest hit of the
 // shadow ray (tmin 0, tmax inf) is the target triangle at t >= 1e-4.
+// `origin` = the primitive the ray leaves (origin_occludes).
 template <int STACK, int MODE>
-__device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target) {
+__device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
+                                      uint32_t origin) {
   const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
   float tT, u, v;
   if (!tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v)) return false;
   if (!(tT >= kDistanceEpsilon)) return false;
+  if (origin_occludes<MODE>(sc, cx, o, d, origin, target, tT)) return false;
   return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT);
 }
 
@@ -1153,6 +1224,8 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
                                                StampRef st) {
   const uint32_t lane = threadIdx.x & 63u;
   const bool last = (bounce + 1 == a.max_path_length);
+  LS_ADD(14, 1);
+  LS_ADD(15, (uint32_t)__popcll(__ballot(active)));
   // -- phase 0: generate (bounce 0) or load (SoA queue planes 0-1) the ray
   PathState s;
   uint32_t tag = 0;   // tag = global owned slot | prevDiffuse << 31
@@ -1196,6 +1269,8 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
     const uint32_t cnt = hd & 0xFFu;
     if (cnt != kPrimaryFallback) {
       listed = true;
+      LS_ADD(18, 1);
+      LS_ADD(19, (uint32_t)__popcll(__ballot(active)));
       if (active) primary_nearest<MODE>(sc, cx, a.primary + (hd >> 8), cnt, s.o, s.d, h);
     }
   }
@@ -1222,6 +1297,10 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   const bool hit_ok = active && h.found && !(h.t < kDistanceEpsilon);
   ShadowRay sh;
   sh.valid = false;
+  if (__ballot(hit_ok)) {
+    LS_ADD(12, 1);
+    LS_ADD(13, (uint32_t)__popcll(__ballot(hit_ok)));
+  }
   if (hit_ok) {
     const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;   // frame in batch
     uint32_t x, y;
@@ -1270,7 +1349,11 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   }
   STAMP_AT(st, 3);
   // -- phase 4: shadow ray (MPS intersect :545-553 + lightSamplingHandler :214-231)
-  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target))) {
+  if (__ballot(sh.valid)) {
+    LS_ADD(16, (uint32_t)__popcll(__ballot(sh.valid)));
+    LS_ADD(17, 1);
+  }
+  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target, h.prim))) {
     s.R = add(s.R, sh.L);
   }
   if (alive && !(a.debug & 4u)) out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
@@ -1295,6 +1378,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   __shared__ uint32_t s_cursor[2], s_res, s_closed;
   STAMP_ENTRY();
   span_begin(a);
+  LS_INIT();
   const uint32_t tid = threadIdx.x;
   const uint32_t G = gridDim.x;
   const uint32_t nseg = (a.bounce == 0) ? 0u : a.in_segments;
@@ -1409,6 +1493,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
     if (total) atomicAdd(a.out_total, total);   // stats: one atomic per block per launch
     if (blockIdx.x == 0) *a.out_chunk = cap;
   }
+  LS_FLUSH();
   span_end(a);
 }
 
@@ -1439,6 +1524,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
   __shared__ uint32_t s_alive[kBlock / 64][kStreamMaxL];  // survivors per bounce (stats)
   __shared__ uint32_t s_closed;
   span_begin(a);
+  LS_INIT();
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t L = a.max_path_length;
   const LdsCtx cx = stage_lds<MODE>(sc, 0, a.stack_spill);
@@ -1515,6 +1601,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
     // release/acquire fence instead (measured within +0.5 % here, DESIGN.md
     // §2.1a).
     if (!camera) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LS_ADD(camera ? 26 : 27, 1);
     const uint32_t wrote = bounce_wave<STACK, MODE, true>(sc, cx, a, camera ? 0u : lvl, active, idx, slot,
                                                                  a.in_q, a.in_q, nullptr, out, 0u, lanes_below, st);
     if (lvl + 1u < L && lane == 0) {
@@ -1525,6 +1612,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
   // stats: survivors of bounce b = rays alive at the start of bounce b + 1
   for (uint32_t b = lane; b + 1 < L; b += 64u)
     if (s_alive[wave][b]) atomicAdd(a.bounce_counts + b, s_alive[wave][b]);
+  LS_FLUSH();
   span_end(a);
 }
 
@@ -1551,6 +1639,9 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
                                            Hit& h, bool any, uint32_t target, bool& occluded, Trav& tr,
                                            uint32_t* uv = nullptr) {
   while (tr.node != kDone && tr.node >= 0) {
+    LS_ADD(2, 1);
+    LS_ADD(3, (uint32_t)__popcll(__ballot(!any)));
+    LS_ADD(9, (uint32_t)__popcll(__ballot(any)));
     tr.node = interior_step<STACK, MODE, false>(sc, cx, tr.node, o, rb, 0.0f, h.t, tr.sp);
     if (tr.node < 0 && tr.leaf == 0) {
       tr.leaf = tr.node;
@@ -1559,6 +1650,9 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
     if ((uint32_t)__popcll(__ballot(tr.leaf == 0)) <= (uint32_t)MRT_PATH_SLACK) break;
   }
   while (tr.leaf < 0) {
+    LS_ADD(4, 1);
+    LS_ADD(5, (uint32_t)__popcll(__ballot(!any)));
+    LS_ADD(11, (uint32_t)__popcll(__ballot(any)));
     const uint32_t lr = ~(uint32_t)tr.leaf;
     const uint32_t first = lr >> kLeafCountBits, cnt = (lr & (kMaxLeafSize - 1)) + 1;
     if (leaf_tests<MODE>(sc, cx, o, d, 0.0f, first, cnt, h, any, target, uv)) {   // occluded: the query is over
@@ -1611,6 +1705,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   __shared__ uint32_t s_closed;
   __shared__ uint32_t s_count[64];   // rays alive at the start of bounce b + 1 (stats)
   span_begin(a);
+  LS_INIT();
   const uint32_t tid = threadIdx.x;
   const LdsCtx cx = stage_lds<MODE>(sc, 1, a.stack_spill);
   if (tid == 0) s_closed = 0;
@@ -1635,6 +1730,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   uint32_t target = 0;
 
   for (;;) {
+    LS_ADD(25, 1);
     // ---- refill idle lanes with new camera rays (rayGenerator, Shaders.metal:75-103)
     for (;;) {
       const uint64_t idle = __ballot(phase == 0);
@@ -1662,6 +1758,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       }
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
       const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool_next);
+      LS_ADD(24, (uint32_t)__popcll(__ballot(phase == 0 && rank < take)));
       if (phase == 0 && rank < take) {
         const uint32_t idx = pool_next + rank;
         const uint32_t fj = a.batch == 1u ? 0u : idx / a.num_slots;
@@ -1690,6 +1787,8 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       const uint64_t going = __ballot(phase != 0 && !fin);
       if (!going) break;
       if ((uint32_t)__popcll(__ballot(fin)) >= (exhausted ? 1u : (uint32_t)MRT_PATH_SERVICE)) break;
+      LS_ADD(22, 1);
+      LS_ADD(23, (uint32_t)__popcll(going));
       if (phase != 0 && !fin) {
         const RayBox rb = make_raybox(ro, rd);
         trav_round<STACK, MODE>(sc, cx, ro, rd, rb, h, phase == 2, target, occluded, tr);
@@ -1697,6 +1796,8 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       }
     }
     if (!__any(fin)) continue;
+    LS_ADD(20, 1);
+    LS_ADD(21, (uint32_t)__popcll(__ballot(fin)));
 
     // ---- service: finished shadow queries (MPS nearest hit + lightSamplingHandler,
     //      Shaders.metal:214-231), then the path's next bounce
@@ -1725,6 +1826,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       const bool hit_ok = h.found && !(h.t < kDistanceEpsilon);   // :122-126
       ShadowRay sh;
       sh.valid = false;
+      LS_ADD(13, (uint32_t)__popcll(__ballot(hit_ok)));
       if (hit_ok) {
         const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;
         uint32_t x, y;
@@ -1755,7 +1857,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
           const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
           float tT, u, v;
           if (tri_test(ro, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
-              !(tT < kDistanceEpsilon)) {
+              !(tT < kDistanceEpsilon) && !origin_occludes<MODE>(sc, cx, ro, sh.d, h.prim, sh.target, tT)) {
             shadow = true;
             phase = 2;
             rd = sh.d;   // ro = s.o = sh.o
@@ -1785,6 +1887,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   }
   __syncthreads();
   if (tid < 64 && tid + 1 < L && s_count[tid]) atomicAdd(a.bounce_counts + tid, s_count[tid]);
+  LS_FLUSH();
   span_end(a);
 }
 
@@ -2272,6 +2375,24 @@ hipError_t read_wave_times(unsigned long long* out, size_t n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), std::min(n, (size_t)4 * kStampWaves * kStampFields) * sizeof(unsigned long long));
 #else
   for (size_t k = 0; k < n; ++k) out[k] = 0;
+  return hipSuccess;
+#endif
+}
+
+hipError_t read_lane_stats(unsigned long long* out, size_t n, bool reset) {
+  for (size_t k = 0; k < n; ++k) out[k] = 0;
+#if MRT_LANESTATS
+  unsigned long long v[kLaneStats];
+  hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_lanes), sizeof(v));
+  if (e != hipSuccess) return e;
+  for (size_t k = 0; k < n && k < (size_t)kLaneStats; ++k) out[k] = v[k];
+  if (reset) {
+    for (int k = 0; k < kLaneStats; ++k) v[k] = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_lanes), v, sizeof(v));
+  }
+  return e;
+#else
+  (void)reset;
   return hipSuccess;
 #endif
 }

@@ -100,6 +100,13 @@ struct mrt_scene {
   DevBuf isect_spill;       // stage intersect stack spill for trees deeper than kMaxStack
   mrt::HostScene host;
   mrt::BvhResult bvh;
+  // the shadow-ray occluder tree (occluders.h) as uploaded after the main
+  // tree: node refs rebased by bvh.num_nodes, leaf records by the triangle
+  // count, leaf primitive ids = scene primitives (host copy for check_bvh)
+  std::vector<float> occ_nodes, occ_tris;
+  std::vector<uint32_t> occ_keep;   // primitives the occluder tree holds
+  int32_t occ_root = 0;
+  uint32_t occ_node_base = 0, occ_max_stack = 0;
   DevBuf nodes, tris, prims, materials, lights;
   mrt::DeviceScene dev{};
   mrt_scene_info info{};
@@ -293,6 +300,7 @@ int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
   const int64_t lo = f0 - 2, hi = f0 + (int64_t)n;
   if (r->noise_window.p && lo >= r->noise_first && hi <= r->noise_first + r->noise_count) return MRT_OK;
   const int64_t count = hi - lo;
+  const auto t0 = std::chrono::steady_clock::now();
   std::vector<float> host((size_t)count * mrt::kNoiseFloats);
   const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   std::vector<std::thread> th;
@@ -303,11 +311,15 @@ int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
                               host.data() + (size_t)k * mrt::kNoiseFloats);
     });
   for (auto& x : th) x.join();
+  const auto t1 = std::chrono::steady_clock::now();
   { int rc = finalize_pending(r); if (rc) return rc; }
-  HIP_TRY(hipStreamSynchronize(r->stream));
+  HIP_TRY(hipStreamSynchronize(r->stream));   // (the wait for queued draws is not noise cost)
+  const auto t2 = std::chrono::steady_clock::now();
   HIP_TRY(upload(r->noise_window, host.data(), host.size() * 4));
   r->noise_first = lo;
   r->noise_count = count;
+  r->stats.noise_ms += std::chrono::duration<double, std::milli>((t1 - t0) + (std::chrono::steady_clock::now() - t2)).count();
+  r->stats.noise_tables += (uint64_t)count;
   return MRT_OK;
 }
 
@@ -646,6 +658,12 @@ int mrt_debug_wave_times(uint64_t* out, size_t n) {
   return MRT_OK;
 }
 
+int mrt_debug_lanes(uint64_t* out, size_t n, int reset) {
+  if (!out) return fail(MRT_ERR_INVALID, "null output");
+  HIP_TRY(mrt::fast::read_lane_stats(reinterpret_cast<unsigned long long*>(out), n, reset != 0));
+  return MRT_OK;
+}
+
 int mrt_noise_table(uint64_t seed, int64_t frame, float* out) {
   if (!out) return fail(MRT_ERR_INVALID, "null output");
   mrt::make_noise_table(seed, frame, out);
@@ -814,8 +832,24 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
       f = bitsf(occ.keep[fbits(f)]);
     }
     occ_root = rebase(ob.root);
-    if (ob.num_nodes) up_nodes.insert(up_nodes.end(), ob.nodes.begin(), ob.nodes.begin() + 32 * (size_t)ob.num_nodes);
-    up_tris.insert(up_tris.end(), ob.tris.begin(), ob.tris.end());
+    // the renderer sizes its LDS stack by the deeper of the two trees
+    // (dev.max_stack): an occluder tree deeper than the traversal stack
+    // allows, or deeper than the main tree (it holds a subset of its
+    // triangles, so it would only cost the main tree's stack variant), is
+    // dropped and shadow rays traverse the main tree
+    if (ob.max_stack > (uint32_t)mrt::kMaxTraversalStack || ob.max_stack > s->bvh.max_stack) {
+      occ_on = false;
+      occ_root = mrt::kEmptyChild;
+    } else {
+      if (ob.num_nodes) up_nodes.insert(up_nodes.end(), ob.nodes.begin(), ob.nodes.begin() + 32 * (size_t)ob.num_nodes);
+      up_tris.insert(up_tris.end(), ob.tris.begin(), ob.tris.end());
+      s->occ_nodes.assign(ob.nodes.begin(), ob.nodes.begin() + 32 * (size_t)ob.num_nodes);
+      s->occ_tris = ob.tris;
+      s->occ_keep = occ.keep;
+      s->occ_root = occ_root;
+      s->occ_node_base = node_base;
+      s->occ_max_stack = ob.max_stack;
+    }
   }
   mrt_scene_info& in = s->info;
   if (occ_on) {
@@ -823,6 +857,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     in.occluder_culled = occ.culled;
     in.occluder_nodes = ob.num_nodes;
     in.occluder_margin = occ.margin;
+    in.occluder_max_stack = ob.max_stack;
   }
   in.vertices = (uint32_t)h.vertices.size();
   in.triangles = T;
@@ -897,59 +932,65 @@ int mrt_scene_export(const mrt_scene* scene, void* vertices, void* indices, void
   return MRT_OK;
 }
 
-int mrt_scene_check_bvh(const mrt_scene* scene) {
-  if (!scene) return fail(MRT_ERR_INVALID, "null scene");
-  const mrt::BvhResult& b = scene->bvh;
-  const mrt::HostScene& h = scene->host;
+extern "C++" {
+namespace {
+// Structural check of one BVH4 over the scene's primitives: every primitive
+// in `want` in exactly one leaf (and no other), every child box contains its
+// subtree's triangles, leaf records match the vertices, the stack bound
+// holds.  node(ref) / tri(k) map the tree's (possibly rebased) references to
+// host records; nodes [node_lo, node_lo + num_nodes) must all be reachable.
+template <class NodeFn, class TriFn>
+int check_tree(const mrt::HostScene& h, int32_t root, uint32_t node_lo, uint32_t num_nodes, uint32_t tri_lo,
+               uint32_t tri_count, uint32_t max_stack, const std::vector<uint8_t>& want, NodeFn node, TriFn tri,
+               const char* what) {
   const uint32_t T = (uint32_t)h.references.size();
   std::vector<uint8_t> seen(T, 0);
   auto fbits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
-  // returns false on violation; checks triangle containment in the given box
-  // pend = stack entries pushed by the ancestors (bounded by b.max_stack)
+  auto bad = [&](const char* m) { return fail(MRT_ERR_STATE, std::string(what) + ": " + m); };
+  // pend = stack entries pushed by the ancestors (bounded by max_stack)
   struct Item { int32_t ref; float lo[3], hi[3]; uint32_t depth, pend; };
   std::vector<Item> stack;
-  Item root{b.root, {-1e30f, -1e30f, -1e30f}, {1e30f, 1e30f, 1e30f}, 0, 0};
-  stack.push_back(root);
+  stack.push_back(Item{root, {-1e30f, -1e30f, -1e30f}, {1e30f, 1e30f, 1e30f}, 0, 0});
   uint32_t nodes_seen = 0;
   while (!stack.empty()) {
     Item it = stack.back();
     stack.pop_back();
-    if (it.depth >= (uint32_t)mrt::kMaxTraversalStack) return fail(MRT_ERR_STATE, "BVH too deep");
+    if (it.depth >= (uint32_t)mrt::kMaxTraversalStack) return bad("BVH too deep");
     if (it.ref >= 0) {
-      if ((uint32_t)it.ref >= b.num_nodes) return fail(MRT_ERR_STATE, "BVH node index out of range");
+      if ((uint32_t)it.ref < node_lo || (uint32_t)it.ref - node_lo >= num_nodes) return bad("BVH node index out of range");
       ++nodes_seen;
       Item ch[4];
       uint32_t nc = 0;
       {
-        const float* n = &b.nodes[32 * (size_t)it.ref];
+        const float* n = node((uint32_t)it.ref);
         for (int c = 0; c < 4; ++c) {
           const int32_t ref = (int32_t)fbits(n[24 + c]);
           if (ref == mrt::kEmptyChild) continue;
-          if (nc != (uint32_t)c) return fail(MRT_ERR_STATE, "BVH4 empty slot before a used one");
+          if (nc != (uint32_t)c) return bad("BVH4 empty slot before a used one");
           ch[nc++] = Item{ref, {n[c], n[8 + c], n[16 + c]}, {n[4 + c], n[12 + c], n[20 + c]}, it.depth + 1, 0};
         }
-        if (nc < 2) return fail(MRT_ERR_STATE, "BVH4 node with fewer than two children");
+        if (nc < 2) return bad("BVH4 node with fewer than two children");
       }
       for (uint32_t c = 0; c < nc; ++c) {
         for (int k = 0; k < 3; ++k)
-          if (!(ch[c].lo[k] <= ch[c].hi[k])) return fail(MRT_ERR_STATE, "BVH empty child box");
+          if (!(ch[c].lo[k] <= ch[c].hi[k])) return bad("BVH empty child box");
         ch[c].pend = it.pend + nc - 1;
-        if (ch[c].pend > b.max_stack) return fail(MRT_ERR_STATE, "BVH stack bound too small");
+        if (ch[c].pend > max_stack) return bad("BVH stack bound too small");
         stack.push_back(ch[c]);
       }
     } else {
       const uint32_t leaf = ~(uint32_t)it.ref;
       const uint32_t first = leaf >> mrt::kLeafCountBits, cnt = (leaf & (mrt::kMaxLeafSize - 1)) + 1;
-      if (first + cnt > T) return fail(MRT_ERR_STATE, "BVH leaf range out of bounds");
+      if (first < tri_lo || first - tri_lo + cnt > tri_count) return bad("BVH leaf range out of bounds");
       for (uint32_t k = first; k < first + cnt; ++k) {
-        const float* t = &b.tris[12 * (size_t)k];
+        const float* t = tri(k);
         const uint32_t prim = fbits(t[3]);
-        if (prim >= T || seen[prim]) return fail(MRT_ERR_STATE, "BVH primitive missing or duplicated");
+        if (prim >= T || !want[prim] || seen[prim]) return bad("BVH primitive missing, foreign or duplicated");
         seen[prim] = 1;
         for (int c = 0; c < 3; ++c) {
           const float* p = h.vertices[h.references[prim].tri[c]].v;
           for (int a = 0; a < 3; ++a)
-            if (!(p[a] >= it.lo[a] && p[a] <= it.hi[a])) return fail(MRT_ERR_STATE, "BVH box does not contain its triangle");
+            if (!(p[a] >= it.lo[a] && p[a] <= it.hi[a])) return bad("BVH box does not contain its triangle");
         }
         // leaf record = (v0, prim), (v1 - v0), (v2 - v0)
         const float* v0 = h.vertices[h.references[prim].tri[0]].v;
@@ -957,14 +998,38 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
         const float* v2 = h.vertices[h.references[prim].tri[2]].v;
         for (int a = 0; a < 3; ++a)
           if (t[a] != v0[a] || t[4 + a] != v1[a] - v0[a] || t[8 + a] != v2[a] - v0[a])
-            return fail(MRT_ERR_STATE, "BVH leaf triangle record mismatch");
+            return bad("BVH leaf triangle record mismatch");
       }
     }
   }
   for (uint32_t t = 0; t < T; ++t)
-    if (!seen[t]) return fail(MRT_ERR_STATE, "BVH primitive not referenced");
-  if (nodes_seen != b.num_nodes) return fail(MRT_ERR_STATE, "BVH has unreachable nodes");
+    if (want[t] && !seen[t]) return bad("BVH primitive not referenced");
+  if (nodes_seen != num_nodes) return bad("BVH has unreachable nodes");
   return MRT_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int mrt_scene_check_bvh(const mrt_scene* scene) {
+  if (!scene) return fail(MRT_ERR_INVALID, "null scene");
+  const mrt::BvhResult& b = scene->bvh;
+  const mrt::HostScene& h = scene->host;
+  const uint32_t T = (uint32_t)h.references.size();
+  std::vector<uint8_t> all(T, 1);
+  int rc = check_tree(
+      h, b.root, 0, b.num_nodes, 0, T, b.max_stack, all, [&](uint32_t r) { return &b.nodes[32 * (size_t)r]; },
+      [&](uint32_t k) { return &b.tris[12 * (size_t)k]; }, "main tree");
+  if (rc || scene->occ_keep.empty()) return rc;
+  // the occluder tree: exactly the kept primitives, its own stack bound, which
+  // the renderer's stack (sized by the deeper tree) covers
+  std::vector<uint8_t> kept(T, 0);
+  for (uint32_t p : scene->occ_keep) kept[p] = 1;
+  const uint32_t occ_nodes = (uint32_t)(scene->occ_nodes.size() / 32);
+  if (scene->occ_max_stack > b.max_stack) return fail(MRT_ERR_STATE, "occluder tree: deeper than the main tree");
+  return check_tree(
+      h, scene->occ_root, scene->occ_node_base, occ_nodes, T, (uint32_t)scene->occ_keep.size(), scene->occ_max_stack,
+      kept, [&](uint32_t r) { return &scene->occ_nodes[32 * (size_t)(r - scene->occ_node_base)]; },
+      [&](uint32_t k) { return &scene->occ_tris[12 * (size_t)(k - T)]; }, "occluder tree");
 }
 
 int mrt_scene_destroy(mrt_scene* scene) {
@@ -1186,7 +1251,9 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   // r3, with traversal slack: trees deeper than 32 entries (the 1M-triangle
   // scenes, 48) keep 12 in LDS — C4 +1.9 %; C3 (26) is best at 8 (12: -0.4 %,
   // C3g -0.9 %), and 16 entries lose everywhere (C4 -0.4 %, C3g -2.4 %)
-  const uint32_t need = desc->scene->bvh.max_stack;
+  // the deeper of the main and the occluder tree (dev.max_stack): shadow rays
+  // may traverse either
+  const uint32_t need = desc->scene->dev.max_stack;
   uint32_t cap = need <= 16 ? 16 : (need > 32 ? 12 : 8);
   if (const char* v = std::getenv("MRT_STACK")) cap = std::max<uint32_t>(8, (uint32_t)std::strtoul(v, nullptr, 0));
   const uint32_t want = std::min(need, cap);
@@ -1721,6 +1788,40 @@ int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
   HIP_TRY(hipEventRecord(x.gather_done[i], r->stream));
   x.gather_recorded[i] = true;
   return exchange_unpack(r, i);
+}
+
+// Test entry (include/mrt.h): rank 0's half of the gather exchange without
+// a communicator — `gathered` (host, nranks slabs of slab_floats packed
+// floats, rank k's at k * slab_floats, as ncclGather delivers them) is copied
+// into the receive buffer and unpacked by the same exchange_unpack the RCCL
+// path runs, so slabs k >= 1 of an N-rank gather are exercised on one device.
+int mrt_debug_exchange_unpack(mrt_renderer* r, uint32_t nranks, const float* gathered, size_t floats) {
+  if (!r || !gathered) return fail(MRT_ERR_INVALID, "mrt_debug_exchange_unpack: null argument");
+  if (nranks < 2 || r->desc.shard_count != nranks || r->desc.shard_rank != 0)
+    return fail(MRT_ERR_INVALID, "mrt_debug_exchange_unpack: the renderer must be rank 0 of nranks >= 2");
+  HIP_TRY(hipSetDevice(r->scene->device));
+  int rc = exchange_flush(r);
+  if (rc) return rc;
+  mrt_comm c;   // shape only: exchange_buffers reads rank / nranks
+  c.nranks = nranks;
+  c.rank = 0;
+  c.device = r->scene->device;
+  rc = exchange_buffers(r, &c);
+  if (rc) return rc;
+  Exchange& x = r->x;
+  if (floats != x.slab_floats * nranks) return fail(MRT_ERR_INVALID, "mrt_debug_exchange_unpack: need nranks * slab floats");
+  x.rank = 0;
+  x.nranks = nranks;
+  x.width = r->desc.width;
+  x.height = r->desc.height;
+  r->image_foreign = true;
+  HIP_TRY(hipMemcpyAsync(x.gathered.p, gathered, floats * 4, hipMemcpyHostToDevice, r->stream));
+  HIP_TRY(hipEventRecord(x.gather_done[0], r->stream));   // "the gather is done"
+  x.gather_recorded[0] = true;
+  rc = exchange_unpack(r, 0);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  return MRT_OK;
 }
 
 int mrt_renderer_exchange_flush(mrt_renderer* r) {

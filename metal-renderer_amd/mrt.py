@@ -96,6 +96,7 @@ class SceneInfo(ctypes.Structure):
         ("build_ms", ctypes.c_double), ("device_bytes", ctypes.c_uint64),
         ("occluder_planes", ctypes.c_uint32), ("occluder_culled", ctypes.c_uint32),
         ("occluder_nodes", ctypes.c_uint32), ("occluder_margin", ctypes.c_float),
+        ("occluder_max_stack", ctypes.c_uint32),
     ]
 
 
@@ -120,6 +121,7 @@ class Stats(ctypes.Structure):
         ("timed_launches", ctypes.c_uint64), ("kernel", ctypes.c_uint32), ("inflight", ctypes.c_uint32),
         ("span_ms", ctypes.c_double), ("spans", ctypes.c_uint64),
         ("primary_blocks", ctypes.c_uint32), ("primary_mean", ctypes.c_float),
+        ("noise_ms", ctypes.c_double), ("noise_tables", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -141,6 +143,7 @@ EXPORTED = [
     "mrt_renderer_exchange_flush", "mrt_renderer_tiles_read", "mrt_renderer_tiles_write",
     "mrt_image_load_exr", "mrt_renderer_load_reference", "mrt_renderer_display",
     "mrt_renderer_display_enqueue", "mrt_renderer_display_map",
+    "mrt_debug_lanes", "mrt_debug_exchange_unpack",
 ]
 
 _lib = None
@@ -193,6 +196,8 @@ def lib() -> ctypes.CDLL:
         "mrt_event_destroy": [vp],
         "mrt_debug_stamps": [vp, c_int],
         "mrt_debug_wave_times": [vp, ctypes.c_size_t],
+        "mrt_debug_lanes": [vp, ctypes.c_size_t, c_int],
+        "mrt_debug_exchange_unpack": [vp, u32, vp, ctypes.c_size_t],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
         "mrt_tiles_packed_floats": [u32, u32, u32, u32, ctypes.POINTER(u64)],
         "mrt_display": [vp, vp, vp, u32, u32, u32, ctypes.c_float, vp],
@@ -426,6 +431,16 @@ class Renderer:
         _check(lib().mrt_renderer_tiles_write(self._h, shard_rank, ctypes.c_void_p(packed.ctypes.data), packed.size),
                "mrt_renderer_tiles_write")
 
+    def debug_exchange_unpack(self, nranks: int, gathered) -> None:
+        """Test entry: rank 0's unpack of an nranks-way gather whose received
+        buffer is `gathered` (host float32, nranks slabs of
+        tiles_packed_floats(W, H, 0, nranks) floats) — the RCCL path's unpack
+        of slabs 1..N-1 without a communicator."""
+        import numpy as np
+        g = np.ascontiguousarray(gathered, np.float32)
+        _check(lib().mrt_debug_exchange_unpack(self._h, nranks, ctypes.c_void_p(g.ctypes.data), g.size),
+               "mrt_debug_exchange_unpack")
+
     # ---- golden comparison (loadReferenceImage + blitFragment) ----
     def load_reference(self, path: str) -> None:
         _check(lib().mrt_renderer_load_reference(self._h, path.encode()), "mrt_renderer_load_reference")
@@ -601,6 +616,15 @@ def debug_stamps(reset: bool = True):
     import numpy as np
     out = np.zeros(8, np.uint64)
     _check(lib().mrt_debug_stamps(ctypes.c_void_p(out.ctypes.data), int(reset)), "mrt_debug_stamps")
+    return out
+
+
+def debug_lanes(reset: bool = True):
+    """Lane-occupancy counters of the lane-statistics library (zeros in the
+    product library); tools/lane_stats.py names the slots."""
+    import numpy as np
+    out = np.zeros(64, np.uint64)
+    _check(lib().mrt_debug_lanes(ctypes.c_void_p(out.ctypes.data), out.size, int(reset)), "mrt_debug_lanes")
     return out
 
 

@@ -95,6 +95,45 @@ def test_host_tiles_roundtrip(gpu, mrt_mod):
     assert got[..., :3].tobytes() == ref[..., :3].tobytes()
 
 
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_rank0_unpacks_gathered_slabs(gpu, mrt_mod, n):
+    """Rank 0's unpack of an N-rank ncclGather (renderer.cpp exchange_unpack:
+    slab k at k * slab_floats, tile k*count + k-th of rank k) on one device:
+    the receive buffer is filled with N synthetic packed slabs through the
+    test entry mrt_debug_exchange_unpack, and the image must equal rank 0's
+    own render with every other rank's tiles written by tiles_unpack_host,
+    bitwise.  Slab 0 (rank 0's own tiles, never unpacked) is poisoned."""
+    W, H = 3840, 2160
+    sc = mrt_mod.Scene("cornellbox", device=0)
+    r = mrt_mod.Renderer(sc, W, H, 1, shard_rank=0, shard_count=n)
+    r.draw(1)
+    expect = r.read_image()
+    slab = mrt_mod.tiles_packed_floats(W, H, 0, n)
+    gathered = np.zeros(n * slab, np.float32)
+    gathered[:slab] = np.nan
+    rng = np.random.default_rng(1000 + n)
+    for k in range(1, n):
+        m = mrt_mod.tiles_packed_floats(W, H, k, n)
+        assert m <= slab
+        data = rng.standard_normal(m).astype(np.float32)
+        gathered[k * slab:k * slab + m] = data
+        mrt_mod.tiles_unpack_host(data.reshape(-1, 64, 64, 4), expect, k, n)
+    r.debug_exchange_unpack(n, gathered)
+    got = r.read_image()
+    r.close()
+    assert got.tobytes() == expect.tobytes()
+    # every pixel of the frame is rank 0's or came from a slab
+    own = np.zeros((H, W), bool)
+    mask = np.zeros((H, W), np.uint8)
+    for k in range(n):
+        mask[:] = 0
+        mrt_mod.tiles_unpack_host(np.ones((mrt_mod.tiles_packed_floats(W, H, k, n) // 16384, 64, 64, 1), np.uint8),
+                                  mask[..., None], k, n)
+        assert not (own & mask.astype(bool)).any()
+        own |= mask.astype(bool)
+    assert own.all()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
