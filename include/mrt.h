@@ -111,6 +111,8 @@ typedef struct mrt_scene_info {
   uint32_t occluder_max_stack;     /* traversal stack entries the occluder tree can need (<= bvh_max_stack:
                                       a deeper occluder tree is not built); renderers size their stack by
                                       the deeper tree.  ABI 7. */
+  float occluder_cos_min;          /* shadow rays whose cosine to the target light's normal is below this
+                                      traverse the main tree (bound on the light's own t error). ABI 7. */
 } mrt_scene_info;
 
 int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out);

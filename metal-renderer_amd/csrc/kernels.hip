@@ -717,10 +717,12 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
 
 // The tree a shadow ray from o traverses: the occluder tree when o is inside
 // every culled plane by the margin (occluders.h: no triangle of those planes
-// can then stand between o and a light), else the main tree.  The plane data
+// can then stand between o and a light) and the ray does not graze the
+// light's plane (`graze`: cosine below occ_cos_min, where the light's own t
+// error could reach a culled crossing), else the main tree.  The plane data
 // is wave-uniform (kernel argument, scalar registers).
-__device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o) {
-  if (sc.occ_planes == 0) return sc.root;
+__device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o, bool graze) {
+  if (sc.occ_planes == 0 || graze) return sc.root;
   bool inside = true;
   for (uint32_t k = 0; k < sc.occ_planes; ++k) {
     const float* p = sc.occ_plane[k];
@@ -731,11 +733,11 @@ __device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o) {
 
 template <int STACK, int MODE>
 __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                                               float t_target) {
+                                               float t_target, bool graze) {
   Hit h;
   h.t = t_target;
   h.found = false;
-  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, shadow_root(sc, o));
+  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, shadow_root(sc, o, graze));
 }
 
 // The shadow ray's own surface first (exact early-out, r4).  The occlusion
@@ -773,14 +775,14 @@ __device__ __forceinline__ bool origin_occludes(const DeviceScene& sc, const Lds
 // `origin` = the primitive the ray leaves (origin_occludes).
 template <int STACK, int MODE>
 __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                                      uint32_t origin) {
+                                      uint32_t origin, bool graze) {
   const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
   float tT, u, v;
   if (!tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v)) return false;
   if (!(tT >= kDistanceEpsilon)) return false;
   if (origin_occludes<MODE>(sc, cx, o, d, origin, target, tT)) return false;
-  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT);
+  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT, graze);
 }
 
 // ---------------------------------------------------------------------------
@@ -902,11 +904,11 @@ __device__ __forceinline__ V3 generateNextBounce(const Mat& m, V3 wI, float curr
 
 // lightTriangleSamplePDF — KernelHelpers.h:181-190
 __device__ __forceinline__ float lightTriangleSamplePDF(float tpdf, float area, V3 source, V3 sv, V3 sn,
-                                                        V3& dirOut) {
+                                                        V3& dirOut, float& LdotD) {
   const V3 d = sub(sv, source);
   const float dist = length(d);
   dirOut = normalize(d);
-  const float LdotD = -dot(dirOut, sn);
+  LdotD = -dot(dirOut, sn);
   const float valid = float(dist >= kDistanceEpsilon) * float(LdotD >= kAngleEpsilon);
   return valid * tpdf * triangleSamplePDF(area, LdotD, dist);
 }
@@ -940,6 +942,7 @@ struct ShadowRay {
   V3 o, d, L;
   uint32_t target;
   bool valid;
+  bool graze;   // cosine to the light below the occluder tree's guard (shadow_root)
 };
 
 // rayGenerator — renderer/Shaders.metal:75-103 (camera fixed at t = 0)
@@ -952,7 +955,7 @@ __device__ __forceinline__ void camera_ray(uint32_t x, uint32_t y, uint32_t W, u
   const float ncx = m_div(float(2 * x), wm1) - 1.0f;
   const float ncy = m_div(float(2 * y), hm1) - 1.0f;
   d = normalize(mk(dudvx + ncx, dudvy + ncy * aspect, -1.0f));
-  o = mk(0.0f, 1.0f, 2.35f);   // up - view * 2.35
+  o = mk(kCameraX, kCameraY, kCameraZ);   // up - view * 2.35
 }
 
 // Owned slots: slot s of a frame = owned tile k = s >> 12 (global tile
@@ -1014,6 +1017,7 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
     s.R = mk(f, f, f);
   }
   sh.valid = false;
+  sh.graze = true;
   // light sampling — Shaders.metal:150-176
   if (bounce + 1 < L) {
     const uint32_t li = selectLightTriangle<MODE>(sc, cx, sc.num_lights, ns.z);
@@ -1039,7 +1043,9 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
     MRT_SHADE_BARRIER();
     const float4 LA = fetch_light<MODE>(sc, cx, li, 0);
     V3 dirToLight;
-    const float lightPdf = lightTriangleSamplePDF(lpdf, LA.w, hv, lv, ln, dirToLight);
+    float cosL;
+    const float lightPdf = lightTriangleSamplePDF(lpdf, LA.w, hv, lv, ln, dirToLight, cosL);
+    sh.graze = !(cosL >= sc.occ_cos_min);
     float materialBsdf, materialPdf;
     sampleMaterial(m, wI, dirToLight, hn, ns, materialBsdf, materialPdf);
     const float weight = balanceHeuristic(lightPdf, materialPdf);
@@ -1056,8 +1062,9 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
   if (light_index != 0xFFFFFFFFu) {
     const float area = fetch_light<MODE>(sc, cx, light_index, 0).w, tpdf = fetch_light<MODE>(sc, cx, light_index, 1).w;
     V3 dirToLight;
+    float cosE;
     const float mPdf = s.pdf;
-    const float lPdf = s.prevDiffuse * lightTriangleSamplePDF(tpdf, area, s.o, hv, hn, dirToLight);
+    const float lPdf = s.prevDiffuse * lightTriangleSamplePDF(tpdf, area, s.o, hv, hn, dirToLight, cosE);
     const float weight = balanceHeuristic(mPdf, lPdf);
     const float k = weight * mPdf;
     s.R = add(s.R, mk((m.le.x * s.T.x) * k, (m.le.y * s.T.y) * k, (m.le.z * s.T.z) * k));
@@ -1353,7 +1360,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
     LS_ADD(16, (uint32_t)__popcll(__ballot(sh.valid)));
     LS_ADD(17, 1);
   }
-  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target, h.prim))) {
+  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target, h.prim, sh.graze))) {
     s.R = add(s.R, sh.L);
   }
   if (alive && !(a.debug & 4u)) out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
@@ -1861,7 +1868,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
             shadow = true;
             phase = 2;
             rd = sh.d;   // ro = s.o = sh.o
-            trav_begin(shadow_root(sc, ro), tr);
+            trav_begin(shadow_root(sc, ro, sh.graze), tr);
             h.t = tT;
             h.u = sh.L.x;
             h.v = sh.L.y;

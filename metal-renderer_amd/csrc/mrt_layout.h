@@ -23,6 +23,9 @@ namespace mrt {
 constexpr float kDistanceEpsilon = 0.0001f;          // DISTANCE_EPSILON
 constexpr float kAngleEpsilon = 0.00003807693583f;   // ANGLE_EPSILON
 constexpr float kPi = 3.1415926f;                    // PI (truncated, as in the reference)
+// rayGenerator's fixed camera origin up - view * 2.35 (renderer/Shaders.metal:75-103),
+// shared by the kernels' camera_ray and the candidate-list builder (primary.cpp)
+constexpr float kCameraX = 0.0f, kCameraY = 1.0f, kCameraZ = 2.35f;
 constexpr unsigned kNoiseDim = 64;                   // NOISE_DIMENSIONS
 constexpr unsigned kNoiseFloats = kNoiseDim * kNoiseDim * 4;
 constexpr unsigned kTile = 64;                       // shard tile edge (== NOISE_DIMENSIONS)
@@ -109,6 +112,8 @@ struct DeviceScene {
   uint32_t occ_tris;
   uint32_t occ_planes;
   float occ_margin;
+  float occ_cos_min;         // ... and whose cosine to the target light's (interpolated) normal is at least
+                             // this (grazing guard for the light's own t error, occluders.cpp)
   float occ_plane[8][4];
 };
 constexpr uint32_t kMaxOccPlanes = 8;

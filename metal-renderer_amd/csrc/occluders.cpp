@@ -11,8 +11,24 @@
 // |n.d| |e1 x e2|.  With c = |e1||e2| / |e1 x e2| (1 / sin of T's angle at v0),
 // S >= |s|, t_q and the scene diagonal, a margin d >= 128 u c S keeps the
 // numerator's sign and keeps a crossing beyond q (relative distance
-// d_q / d_p from q) beyond the computed t_q for every direction; a grazing
+// d_q / d_p from q) beyond the true t_q for every direction; a grazing
 // direction gives |t| > 6 S > t_q.  Triangles with c > 16 (slivers) are kept.
+//
+// The light's own t_q (the target test, kernels.hip tri_test) is computed
+// too: by the same analysis its error is about 10 u S c_L / |cos_L| (c_L the
+// light triangle's c, cos_L the ray's cosine to the light's plane), which
+// grows without bound for rays grazing the light plane (the reference only
+// asks cos_L >= ANGLE_EPSILON, 3.8e-5).  A computed t_q above the true one
+// could then reach a culled crossing.  The distance from q to a culled plane
+// along the ray is at least D_L (the light vertices' least distance inside the
+// culled planes), so the crossing stays beyond the computed t_q whenever the
+// culled triangles' error (covered by margin, D_L >= 4 margin is required)
+// plus the light's error stays below D_L: the kernels use the occluder tree
+// only for shadow rays with cos_L >= cos_min = 20 u S c_L / D_L (light error
+// <= D_L / 2), taken against the interpolated light normal the kernels
+// already compute, so cos_min also adds twice the largest deviation of a
+// light vertex normal from its triangle's geometric normal (ANGLE below).
+// Rays under cos_min (a negligible share) traverse the main tree.
 #include "occluders.h"
 
 #include <algorithm>
@@ -44,7 +60,8 @@ constexpr double kUnit = 5.9604644775390625e-08;   // 2^-24
 }  // namespace
 
 bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_vertices, const uint32_t* indices,
-                    uint32_t num_triangles, const float* light_vertices, uint32_t num_lights, OccluderSet& out) {
+                    uint32_t num_triangles, const float* light_vertices, const float* light_normals,
+                    uint32_t num_lights, OccluderSet& out) {
   out = OccluderSet{};
   if (num_triangles == 0 || num_triangles > kMaxClassifiedTriangles || num_vertices == 0) return false;
   const size_t stride = stride_bytes / sizeof(float);
@@ -115,14 +132,15 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
   double c_all = 1.0, dev_all = 0.0;
   for (const Plane& P : planes) { c_all = std::max(c_all, P.c_max); dev_all = std::max(dev_all, P.dev); }
   const double margin = 128.0 * kUnit * c_all * S + dev_all + 8.0 * kUnit * S;
-  // every light vertex strictly inside (by twice the margin); planes holding a
-  // light triangle (or too close to one) keep their triangles
+  // every light vertex strictly inside (by four margins: two for the culled
+  // triangles' error, two left for the light's, see cos_min); planes holding
+  // a light triangle (or too close to one) keep their triangles
   std::vector<Plane> used;
   for (Plane& P : planes) {
     bool ok = true;
     for (uint32_t l = 0; l < num_lights * 3 && ok; ++l) {
       const float* q = light_vertices + 3 * l;
-      if (!(dot(P.n, D3{q[0], q[1], q[2]}) - P.w <= -2.0 * margin)) ok = false;
+      if (!(dot(P.n, D3{q[0], q[1], q[2]}) - P.w <= -4.0 * margin)) ok = false;
     }
     if (ok) used.push_back(std::move(P));
   }
@@ -141,6 +159,39 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
   // the float plane differs from the double one by rounding: covered by the
   // runtime check's 8 u S term
   out.margin = (float)margin;
+  // the grazing guard (header comment): D_L over the planes used, c_L and the
+  // normal deviation over the light triangles
+  double D_L = 1e300, c_L = 1.0, ndev = 0.0;
+  for (const Plane& P : used)
+    for (uint32_t l = 0; l < num_lights * 3; ++l) {
+      const float* q = light_vertices + 3 * l;
+      D_L = std::min(D_L, P.w - dot(P.n, D3{q[0], q[1], q[2]}));
+    }
+  for (uint32_t l = 0; l < num_lights; ++l) {
+    const float* q = light_vertices + 9 * (size_t)l;
+    const D3 a{q[0], q[1], q[2]}, b{q[3], q[4], q[5]}, c{q[6], q[7], q[8]};
+    const D3 ng0 = cross(sub(b, a), sub(c, a));
+    const double A = len(ng0);
+    if (!(A > 0.0)) { out = OccluderSet{}; return false; }   // degenerate light: no culling
+    const D3 ng = {ng0.x / A, ng0.y / A, ng0.z / A};
+    const D3 v[3] = {a, b, c};
+    for (int k = 0; k < 3; ++k)   // c at each vertex (tri_test takes the triangle's first vertex as v0)
+      c_L = std::max(c_L, len(sub(v[(k + 1) % 3], v[k])) * len(sub(v[(k + 2) % 3], v[k])) / A);
+    for (int k = 0; k < 3; ++k) {
+      const float* nv = light_normals + 9 * (size_t)l + 3 * k;
+      const D3 n{nv[0], nv[1], nv[2]};
+      const double nl = len(n);
+      if (!(nl > 0.0)) { out = OccluderSet{}; return false; }
+      // either orientation of the geometric normal (the kernels use |cos|)
+      const D3 u{n.x / nl, n.y / nl, n.z / nl};
+      ndev = std::max(ndev, std::min(len(sub(u, ng)), len(sub(u, D3{-ng.x, -ng.y, -ng.z}))));
+    }
+  }
+  if (!(D_L > 0.0) || D_L > 1e299) { out = OccluderSet{}; return false; }
+  // + 1e-5: the kernels' float cosine (a normalised interpolated normal and
+  // direction, a few u) with room to spare
+  out.cos_min = (float)(20.0 * kUnit * S * c_L / D_L + 2.0 * ndev + 1e-5);
+  if (!(out.cos_min < 0.5f)) { out = OccluderSet{}; return false; }   // too few rays would qualify
   // a second tree pays only when it is markedly smaller than the main one:
   // it costs a plane test per shadow ray and its own nodes in LDS / L2
   if ((size_t)out.culled * kMinCulledFraction < num_triangles) {

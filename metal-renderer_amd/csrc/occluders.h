@@ -29,14 +29,18 @@ struct OccluderSet {
   std::vector<uint32_t> keep;                  // triangles that stay in the occluder tree (ascending)
   std::vector<std::array<float, 4>> planes;    // culled planes (n, w): inside is n.x - w <= -margin
   float margin = 0.0f;                         // runtime inside margin (scene units)
+  float cos_min = 0.0f;                        // shadow rays with |cos| to the light's normal below this
+                                               //   traverse the main tree (grazing guard, occluders.cpp)
   uint32_t culled = 0;                         // triangles left out
 };
 
-// positions: 3 floats per vertex at `stride_bytes`; light_vertices: 9 floats
-// (three positions) per light triangle.  Returns false (no culling) when the
+// positions: 3 floats per vertex at `stride_bytes`; light_vertices and
+// light_normals: 9 floats (three positions / vertex normals) per light
+// triangle.  Returns false (no culling) when the
 // scene is too large to classify or the qualifying planes hold less than an
 // eighth of the triangles (then `out` is empty).
 bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_vertices, const uint32_t* indices,
-                    uint32_t num_triangles, const float* light_vertices, uint32_t num_lights, OccluderSet& out);
+                    uint32_t num_triangles, const float* light_vertices, const float* light_normals,
+                    uint32_t num_lights, OccluderSet& out);
 
 }  // namespace mrt

@@ -63,7 +63,7 @@ bool build_primary_lists(const float* tris, uint32_t num_tris, uint32_t W, uint3
   const uint32_t BX = (W + kPrimaryBlock - 1) / kPrimaryBlock, BY = (H + kPrimaryBlock - 1) / kPrimaryBlock;
   const uint64_t nblocks = (uint64_t)BX * BY;
   const double W1 = W - 1.0, H1 = H - 1.0, aspect = (double)H / (double)W;
-  const D3 O = {0.0, 1.0, (double)2.35f};   // camera_ray's origin (float 2.35)
+  const D3 O = {(double)kCameraX, (double)kCameraY, (double)kCameraZ};   // camera_ray's origin (mrt_layout.h)
   // rectangle of block (bx, by): pixel centres x0..x1, y0..y1 plus the jitter
   auto rect = [&](uint32_t bx, uint32_t by) {
     const double px0 = bx * kPrimaryBlock, px1 = std::min<double>(px0 + kPrimaryBlock - 1, W - 1.0);

@@ -799,12 +799,14 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   bool occ_on = builder == MRT_BVH_HOST_SAH && !desc->no_occluder_tree;
   if (const char* v = std::getenv("MRT_OCCLUDERS")) occ_on = occ_on && std::atoi(v) != 0;
   if (occ_on) {
-    std::vector<float> lv;
+    std::vector<float> lv, ln;
     for (uint32_t l = 0; l < h.light_count; ++l)
-      for (const mrt::RefVertex* v : {&h.lights[l].v1, &h.lights[l].v2, &h.lights[l].v3})
+      for (const mrt::RefVertex* v : {&h.lights[l].v1, &h.lights[l].v2, &h.lights[l].v3}) {
         lv.insert(lv.end(), {v->v[0], v->v[1], v->v[2]});
+        ln.insert(ln.end(), {v->n[0], v->n[1], v->n[2]});
+      }
     occ_on = mrt::find_occluders(h.vertices.data()->v, sizeof(mrt::RefVertex), (uint32_t)h.vertices.size(),
-                                 h.indices.data(), T, lv.data(), h.light_count, occ);
+                                 h.indices.data(), T, lv.data(), ln.data(), h.light_count, occ);
   }
   const uint32_t node_base = (uint32_t)(s->bvh.nodes.size() / 32), tri_base = T;
   int32_t occ_root = mrt::kEmptyChild;
@@ -858,6 +860,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     in.occluder_nodes = ob.num_nodes;
     in.occluder_margin = occ.margin;
     in.occluder_max_stack = ob.max_stack;
+    in.occluder_cos_min = occ.cos_min;
   }
   in.vertices = (uint32_t)h.vertices.size();
   in.triangles = T;
@@ -904,6 +907,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     d.occ_tris = (uint32_t)occ.keep.size();
     d.occ_planes = (uint32_t)occ.planes.size();
     d.occ_margin = occ.margin;
+    d.occ_cos_min = occ.cos_min;
     for (uint32_t k = 0; k < d.occ_planes; ++k)
       for (int c = 0; c < 4; ++c) d.occ_plane[k][c] = occ.planes[k][c];
     d.max_stack = std::max(d.max_stack, ob.max_stack);

@@ -96,7 +96,7 @@ class SceneInfo(ctypes.Structure):
         ("build_ms", ctypes.c_double), ("device_bytes", ctypes.c_uint64),
         ("occluder_planes", ctypes.c_uint32), ("occluder_culled", ctypes.c_uint32),
         ("occluder_nodes", ctypes.c_uint32), ("occluder_margin", ctypes.c_float),
-        ("occluder_max_stack", ctypes.c_uint32),
+        ("occluder_max_stack", ctypes.c_uint32), ("occluder_cos_min", ctypes.c_float),
     ]
 
 

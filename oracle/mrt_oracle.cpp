@@ -393,7 +393,14 @@ static float half_area(const float* lo, const float* hi) {
   return dx * dy + dy * dz + dz * dx;
 }
 
-static uint32_t build_node(const Scene& sc, std::vector<BuildRef>& refs, uint32_t b, uint32_t e) {
+// Depth bound: below kSahDepth every split is a median split of the range,
+// so a tree is at most kSahDepth + 32 levels deep (< 2^32 primitives) and
+// intersect_bvh's fixed stack of kCpuStack entries (one push per level) never
+// overflows, whatever the SAH would do on a degenerate procedural scene.
+constexpr uint32_t kSahDepth = 90, kCpuStack = 128;
+static_assert(kSahDepth + 32 <= kCpuStack, "oracle BVH stack");
+
+static uint32_t build_node(const Scene& sc, std::vector<BuildRef>& refs, uint32_t b, uint32_t e, uint32_t depth) {
   const uint32_t node = (uint32_t)sc.bvh.size();
   sc.bvh.push_back(CpuBvhNode{});
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -412,6 +419,14 @@ static uint32_t build_node(const Scene& sc, std::vector<BuildRef>& refs, uint32_
     return node;
   };
   if (n <= 4) return make_leaf();
+  if (depth >= kSahDepth) {   // median split (depth bound above)
+    const uint32_t mid = b + n / 2;
+    build_node(sc, refs, b, mid, depth + 1);
+    const uint32_t right = build_node(sc, refs, mid, e, depth + 1);
+    sc.bvh[node].right_or_first = right;
+    sc.bvh[node].count = 0;
+    return node;
+  }
   // 16-bin SAH on the centroid bounds' longest axis
   int axis = 0;
   for (int a = 1; a < 3; ++a) if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
@@ -443,8 +458,8 @@ static uint32_t build_node(const Scene& sc, std::vector<BuildRef>& refs, uint32_
                                     [&](const BuildRef& r) { return bin_of(r) < split; }) - refs.begin());
     if (mid == b || mid == e) mid = b + n / 2;
   }
-  build_node(sc, refs, b, mid);   // left child = node + 1
-  const uint32_t right = build_node(sc, refs, mid, e);
+  build_node(sc, refs, b, mid, depth + 1);   // left child = node + 1
+  const uint32_t right = build_node(sc, refs, mid, e, depth + 1);
   sc.bvh[node].right_or_first = right;
   sc.bvh[node].count = 0;
   return node;
@@ -465,7 +480,7 @@ static void build_cpu_bvh(const Scene& sc) {
   }
   sc.bvh.reserve(T);
   sc.bvh_prims.reserve(T);
-  if (T) build_node(sc, refs, 0, (uint32_t)T);
+  if (T) build_node(sc, refs, 0, (uint32_t)T, 0);
 }
 
 static inline float safe_inv(float d) { return 1.0f / (std::fabs(d) > 1e-20f ? d : std::copysign(1e-20f, d)); }
@@ -492,7 +507,7 @@ static Intersection intersect_bvh(const Scene& sc, const float* o3, float tmin, 
     tn = t0;
     return t0 <= t1;
   };
-  uint32_t stack[128];
+  uint32_t stack[kCpuStack];   // <= depth entries (build_node's bound)
   int sp = 0;
   uint32_t node = 0;
   float tn0;

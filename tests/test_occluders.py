@@ -13,6 +13,8 @@ ceiling the light hangs under.  (The GPU tests check the renders: precise
 build bit-identical to the oracle, which has no occluder tree, and fast
 build bitwise equal with the tree on and off.)
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -138,6 +140,114 @@ def test_culled_triangles_never_occlude(mrt_mod, fma):
     tT, ok = _tri_t(o, d, tv0, Pv[tgt, 1] - tv0, Pv[tgt, 2] - tv0, fma)
     o, d, tT = o[ok], d[ok], tT[ok]
     assert len(o) > n // 3
+    for t in np.nonzero(culled)[0]:
+        v0 = Pv[t, 0]
+        tt, hit = _tri_t(o, d, v0[None], (Pv[t, 1] - v0)[None], (Pv[t, 2] - v0)[None], fma)
+        bad = hit & (tt >= 0) & (tt <= tT)
+        assert not bad.any(), (t, o[bad][:3], d[bad][:3], tt[bad][:3], tT[bad][:3])
+
+
+def _sliver_room(path):
+    """A 2 x 2 x 2 room (floor, ceiling, back and side walls; open front, as
+    the cornellbox), a box in it, and a SLIVER light 0.01 from the left wall,
+    nearly parallel to it: shadow rays toward it graze its plane at every
+    angle, and its triangle's c = |e1||e2| / |e1 x e2| is large."""
+    V, N, F = [], [], []
+
+    def quad(a, b, c, d, n, mtl):
+        k = len(V)
+        V.extend([a, b, c, d])
+        N.append(n)
+        F.append((mtl, [(k + 1, k + 2, k + 3, len(N)), (k + 3, k + 4, k + 1, len(N))]))
+
+    quad((-1, 0, 1), (1, 0, 1), (1, 0, -1), (-1, 0, -1), (0, 1, 0), "white")      # floor
+    quad((-1, 2, -1), (1, 2, -1), (1, 2, 1), (-1, 2, 1), (0, -1, 0), "white")     # ceiling
+    quad((1, 0, -1), (1, 2, -1), (-1, 2, -1), (-1, 0, -1), (0, 0, 1), "white")    # back wall
+    quad((-1, 0, -1), (-1, 2, -1), (-1, 2, 1), (-1, 0, 1), (1, 0, 0), "white")    # left wall
+    quad((1, 0, 1), (1, 2, 1), (1, 2, -1), (1, 0, -1), (-1, 0, 0), "white")      # right wall
+    b = [(-0.3, 0.0, -0.3), (0.3, 0.0, -0.3), (0.3, 0.0, 0.3), (-0.3, 0.0, 0.3)]
+    t = [(x, 0.7, z) for x, _, z in b]
+    quad(t[0], t[3], t[2], t[1], (0, 1, 0), "white")                               # box top
+    for i in range(4):                                                             # box sides
+        j = (i + 1) % 4
+        n = np.cross(np.subtract(t[i], b[i]), np.subtract(b[j], b[i]))
+        quad(b[i], t[i], t[j], b[j], tuple(-n / np.linalg.norm(n)), "white")
+    # the sliver light: long (1.7) and thin (0.02 at its base, c ~ 120 at its tip), 0.01 inside the left wall
+    k = len(V)
+    V.extend([(-0.99, 0.6, -0.6), (-0.99, 1.8, 0.6), (-0.99, 0.6, -0.58)])
+    N.append((1, 0, 0))
+    F.append(("light", [(k + 1, k + 3, k + 2, len(N))]))
+    with open(path, "w") as f:
+        f.write("mtllib sliver.mtl\n")
+        for v in V:
+            f.write("v %.6f %.6f %.6f\n" % v)
+        for n in N:
+            f.write("vn %.6f %.6f %.6f\n" % tuple(n))
+        for mtl, tris in F:
+            f.write(f"usemtl {mtl}\n")
+            for a, b_, c, n in tris:
+                f.write(f"f {a}//{n} {b_}//{n} {c}//{n}\n")
+    with open(os.path.join(os.path.dirname(path), "sliver.mtl"), "w") as f:
+        f.write("newmtl white\nKd 0.8 0.8 0.8\nKs 1.0 0.0 0.0\n\nnewmtl light\nKd 1 1 1\nKs 1.0 0.0 0.0\nKa 20 20 20\n")
+
+
+@pytest.mark.parametrize("fma", [False, True])
+def test_sliver_light_grazing_rays_never_culled_hits(mrt_mod, tmp_path, fma):
+    """the light's own computed t has an error of about
+    10 u S c_L / |cos_L|, unbounded for rays grazing the light's plane, which
+    the culled triangles' margin does not cover.  The library therefore sends
+    shadow rays with cos_L < occluder_cos_min (= 20 u S c_L / D_L + normal
+    deviation) through the main tree.  With a sliver light 0.01 from a culled
+    wall and rays at every angle to it — many within a few degrees of its
+    plane — no culled triangle reports a hit in [0, t_light] for any ray the
+    guard lets through, in the kernels' float32 arithmetic."""
+    path = str(tmp_path / "sliver.obj")
+    _sliver_room(path)
+    s = mrt_mod.Scene(path, device=-1)
+    info = s.info
+    assert info["occluder_planes"] >= 4 and info["occluder_culled"] >= 10
+    cos_min = np.float32(info["occluder_cos_min"])
+    assert 0.01 < cos_min < 0.2   # c_L ~ 120: rays within ~3 degrees of the light's plane are guarded
+    e = s.export()
+    V = e["vertices"]["v"]
+    I = e["indices"]
+    L = e["lights"][:-1]
+    light_pts = np.concatenate([L["v1"]["v"], L["v2"]["v"], L["v3"]["v"]]).astype(np.float64)
+    planes, culled = _supporting_planes(V, I, light_pts)
+    assert culled.sum() == info["occluder_culled"]
+    margin = np.float32(info["occluder_margin"])
+    rng = np.random.default_rng(SEED + 7)
+    n = 200_000
+    lo, hi = V.min(0), V.max(0)
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    # a third of the origins near the light's plane (x = -0.99): grazing rays
+    g = n // 3
+    o[:g, 0] = (np.float32(-0.99) + rng.uniform(-2e-3, 2e-3, g)).astype(np.float32)
+    inside = np.ones(n, bool)
+    for p in planes.astype(np.float32):
+        inside &= (_fma(p[0], o[:, 0], _fma(p[1], o[:, 1], _fma(p[2], o[:, 2], -p[3]))) <= -margin)
+    o = o[inside]
+    li = np.zeros(len(o), np.int64)
+    r1 = np.sqrt(rng.uniform(0, 1, len(o))).astype(np.float32)
+    r2 = rng.uniform(0, 1, len(o)).astype(np.float32)
+    bu, bv, bw = 1 - r1, r1 * (1 - r2), r1 * r2
+    q = (L["v1"]["v"][li] * bu[:, None] + L["v2"]["v"][li] * bv[:, None] + L["v3"]["v"][li] * bw[:, None])
+    q = q.astype(np.float32)
+    d = q - o
+    d = (d / np.sqrt((d * d).sum(1, keepdims=True))).astype(np.float32)
+    # the kernels' cosine to the (interpolated, here constant) light normal
+    ln = (L["v1"]["n"][li] * bu[:, None] + L["v2"]["n"][li] * bv[:, None] + L["v3"]["n"][li] * bw[:, None])
+    ln = (ln / np.sqrt((ln * ln).sum(1, keepdims=True))).astype(np.float32)
+    cosL = -(d * ln).sum(1).astype(np.float32)
+    tgt = L["index"][li]
+    Pv = V[I.reshape(-1, 3)]
+    tv0 = Pv[tgt, 0]
+    tT, ok = _tri_t(o, d, tv0, Pv[tgt, 1] - tv0, Pv[tgt, 2] - tv0, fma)
+    valid = ok & (tT >= np.float32(1e-4)) & (cosL >= np.float32(3.807693583e-05))
+    guarded = valid & (cosL >= cos_min)
+    assert guarded.sum() > 20_000
+    assert (valid & (cosL < cos_min)).sum() > 1_000   # the grazing population the guard sends to the main tree
+    o, d, tT = o[guarded], d[guarded], tT[guarded]
     for t in np.nonzero(culled)[0]:
         v0 = Pv[t, 0]
         tt, hit = _tri_t(o, d, v0[None], (Pv[t, 1] - v0)[None], (Pv[t, 2] - v0)[None], fma)
