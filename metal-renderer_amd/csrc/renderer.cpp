@@ -139,7 +139,7 @@ constexpr int kDrawRing = 3;
 struct FrameSlot {
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  DevBuf queue[2][4];       // ray queues (the streaming wavefront: queue[0] holds the per-wave queues)
+  DevBuf queue[2][mrt::kQueuePlanes];   // ray queues (the streaming wavefront: queue[0] holds the per-wave queues)
   DevBuf segments;          // 2 queues x 2 classes x grid per-block survivor counts + 2 chunk words
   DevBuf radiance;          // W*H float4, written once per owned pixel per frame
   DevBuf spill;             // traversal stack entries beyond the LDS capacity (deep BVHs)
@@ -359,10 +359,18 @@ int alloc_frame_buffers(mrt_renderer* r) {
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
     // the path kernel keeps the path state in LDS: no ray queues; the
     // streaming wavefront needs only its per-wave queues
-    const size_t qslots = r->stream_mode ? mrt::stream_slots(r->desc.max_path_length, r->grid) : slots;
+    // (the stream kernel's queue shape is the loaded build's: 4 or 6 planes)
+    uint32_t planes = 4, planes_p = 4;
+    size_t qslots = slots;
+    if (r->stream_mode) {
+      qslots = std::max(mrt::fast::stream_queue_slots(r->desc.max_path_length, r->grid, &planes),
+                        mrt::precise::stream_queue_slots(r->desc.max_path_length, r->grid, &planes_p));
+      planes = std::max(planes, planes_p);
+    }
     for (int q = 0; q < 2; ++q)
-      for (int p = 0; p < 4; ++p)
-        HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (r->stream_mode && q == 1) ? 0 : qslots * 16));
+      for (int p = 0; p < mrt::kQueuePlanes; ++p)
+        HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (r->stream_mode && q == 1) || (uint32_t)p >= planes ? 0
+                                                                                                      : qslots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
     // spill rows of max_stack words per lane (kernels.hip LdsCtx::spill_lane)
@@ -1443,7 +1451,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.out_chunk = meta + (b & 1);
       a.out_total = cnt + (size_t)k * L + b;
       a.grab = d.counters.as<uint32_t>() + grab_off + ((size_t)k * L + b) * grab_words;
-      for (int p = 0; p < 4; ++p) {
+      for (int p = 0; p < mrt::kQueuePlanes; ++p) {
         a.in_q.plane[p] = fs.queue[b & 1][p].as<float4>();
         a.out_q.plane[p] = fs.queue[(b + 1) & 1][p].as<float4>();
       }

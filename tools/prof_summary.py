@@ -57,10 +57,26 @@ def main(tag="r1", cfg="c2"):
                  if lanes.get("SQ_ACTIVE_INST_VALU") else None)
     bounce = next(r for r in rows if any(k in r["Name"] for k in HOT))
     avg_ns = float(bounce["AverageNs"])
+    # the timed launches alone: the trace's per-dispatch records of the hot
+    # kernel minus the warm-up launches (profile.sh STEPS / WARM; one launch
+    # per step on C1-C5), so the average is comparable with ms_per_step
+    timed_ns, timed_n = None, None
+    trace_csv = os.path.join(src, "trace", "run_kernel_trace.csv")
+    steps_file = os.path.join(src, "steps")
+    if os.path.exists(trace_csv) and os.path.exists(steps_file):
+        steps, warm = (int(x) for x in open(steps_file).read().split())
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace_csv))
+                if r["Kernel_Name"] == bounce["Name"]]
+        if len(durs) >= steps + warm:
+            tail = durs[-steps:]
+            timed_ns, timed_n = sum(tail) / len(tail), len(tail)
     hbm = (2.0 * fetch["FETCH_SIZE"] + write["WRITE_SIZE"]) * 1024.0
     lines = [f"# rocprofv3 summary — {tag} / {cfg}", "",
              "`tools/profile.sh` → kernel trace + stats pass, then separate PMC passes "
-             "(FETCH_SIZE; WRITE_SIZE; SQ; VALU lanes; GRBM), `bench.py --steps 2 --warmup 1`.", "",
+             "(FETCH_SIZE; WRITE_SIZE; SQ; VALU lanes; GRBM), one render stream (MRT_INFLIGHT=1).", "",
+             (f"Hot kernel over the {timed_n} timed launches (warm-up excluded): **{timed_ns / 1e6:.3f} ms per launch** "
+              f"(the stats table below averages every launch, warm-up included)." if timed_ns else
+              "Timed-launch average unavailable (no per-dispatch trace)."), "",
              "| kernel | calls | avg µs | total ms | % |", "|---|---|---|---|---|"]
     for r in rows:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
@@ -78,7 +94,7 @@ def main(tag="r1", cfg="c2"):
               f"* dispatch: {meta}"]
     # VALU issue share: a wave64 VALU instruction occupies its SIMD's issue for
     # 2 cycles (MI355X_MICROARCH.md); capacity = 256 CUs x 4 SIMDs x clock x t
-    clk_hz = clk.get("GRBM_GUI_ACTIVE", 0) / 8 / (avg_ns * 1e-9)
+    clk_hz = clk.get("GRBM_GUI_ACTIVE", 0) / 8 / (avg_ns * 1e-9)   # (PMC passes time every launch alike)
     valu_frac = (2.0 * sq.get("SQ_INSTS_VALU", 0) / (1024 * clk_hz * avg_ns * 1e-9)) if clk_hz else None
     wave_cycles = max(1.0, sq.get("SQ_WAVE_CYCLES", 1.0))
     try:
@@ -102,7 +118,8 @@ def main(tag="r1", cfg="c2"):
         json.dump({"tag": tag, "config": cfg, "kernel": kernel, "commit": commit, "lib_md5": lib_md5,
                    "hbm_bytes_per_launch": round(hbm),
                    "fetch_size_kb": fetch["FETCH_SIZE"], "write_size_kb": write["WRITE_SIZE"],
-                   "avg_launch_ns_rocprof": avg_ns, "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
+                   "avg_launch_ns_rocprof": avg_ns, "avg_launch_ns_rocprof_timed": timed_ns,
+                   "timed_launches_rocprof": timed_n, "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
                    "sq": sq, "clock_ghz": round(clk_hz / 1e9, 3),
                    "valu_issue_frac": None if valu_frac is None else round(valu_frac, 4),
                    "wait_any_frac": round(sq.get("SQ_WAIT_ANY", 0) / wave_cycles, 4),

@@ -14,7 +14,12 @@ OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
 # the library these passes measure (bench.py compares it with the one it loads)
 md5sum metal-renderer_amd/lib/libmrt.so | cut -d' ' -f1 > $OUT/lib.md5
-BENCH="python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline $*"
+# >= 10 timed launches after warm-up: the trace pass's average over the timed
+# launches (prof_summary.py drops the WARM warm-up launches) is the kernel's
+# time per launch on one render stream
+STEPS=${STEPS:-12}; WARM=${WARM:-2}
+echo "$STEPS $WARM" > $OUT/steps
+BENCH="python3 bench.py --config $CFG --steps $STEPS --warmup $WARM --no-cpu-baseline $*"
 set -o pipefail
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1; local rc=$?; tail -n 3 $OUT/$name.log; echo "== $name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -f csv -- $BENCH
