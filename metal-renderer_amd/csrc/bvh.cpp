@@ -385,33 +385,22 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
   }
   // leaf triangle runs in output order of their parents (DFS-ish locality)
   std::vector<int32_t> leaf_ref_of(bn.size(), 0);
-  // 64-B records: a leaf of >= 2 triangles starts at an even record, so its
-  // first pair is one 128-B line (a padding record, prim ~0u, fills the gap)
-  const uint32_t TF = opt.tri_floats == 16 ? 16u : 12u;
-  uint32_t tri_cursor = 0, tri_real = 0;
-  out.tris.clear();
-  out.tris.reserve((size_t)TF * num_triangles * (TF == 16 ? 2 : 1));
+  uint32_t tri_cursor = 0;
+  out.tris.assign(12 * (size_t)num_triangles, 0.0f);
   auto emit_leaf = [&](int32_t id) {
     const BuildNode& n = bn[id];
-    if (TF == 16 && n.count >= 2 && (tri_cursor & 1u)) {
-      out.tris.resize(out.tris.size() + TF, 0.0f);
-      out.tris[out.tris.size() - TF + 3] = bitsf(0xFFFFFFFFu);
-      ++tri_cursor;
-    }
     for (uint32_t i = 0; i < n.count; ++i) {
       const uint32_t prim = b.order[n.first + i];
       const float* v0 = P(indices[3 * prim]);
       const float* v1 = P(indices[3 * prim + 1]);
       const float* v2 = P(indices[3 * prim + 2]);
-      out.tris.resize(out.tris.size() + TF, 0.0f);
-      float* o = &out.tris[out.tris.size() - TF];
+      float* o = &out.tris[12 * (size_t)(tri_cursor + i)];
       o[0] = v0[0]; o[1] = v0[1]; o[2] = v0[2]; o[3] = bitsf(prim);
       o[4] = v1[0] - v0[0]; o[5] = v1[1] - v0[1]; o[6] = v1[2] - v0[2]; o[7] = 0.0f;
       o[8] = v2[0] - v0[0]; o[9] = v2[1] - v0[1]; o[10] = v2[2] - v0[2]; o[11] = 0.0f;
     }
     leaf_ref_of[id] = leaf_ref(tri_cursor, n.count);
     tri_cursor += n.count;
-    tri_real += n.count;
     out.num_leaves++;
   };
   if (is_leaf(0)) {
@@ -474,10 +463,7 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
   (void)fbits;
   out.sah_cost = sah;
   out.max_depth = b.max_depth;
-  if (tri_real != num_triangles) { error = "internal: leaf triangle count mismatch"; return false; }
-  out.tri_floats = TF;
-  out.tri_records = tri_cursor;
-  if ((uint64_t)tri_cursor >= (1ull << (31 - kLeafCountBits))) { error = "too many triangle records"; return false; }
+  if (tri_cursor != num_triangles) { error = "internal: leaf triangle count mismatch"; return false; }
   return true;
 }
 

@@ -29,13 +29,11 @@ struct BvhBuildOptions {
   bool full_sweep = false;        // exact sweep SAH at every node (presorted, O(n log n)); opt-in (MRT_FULL_SWEEP=1)
   float traversal_cost = 1.0f;    // relative to one triangle test
   uint32_t width = 2;             // 2 = the binary SAH tree itself, 4 = BVH4 (128-B nodes, collapsed; what the kernels traverse)
-  uint32_t tri_floats = 12;       // leaf triangle record: 12 floats (48 B) or 16 (64 B: a leaf of two
-                                  // triangles starts at an even record, so it is one 128-B line)
 };
 
 struct BvhResult {
   std::vector<float> nodes;       // 16 (BVH2) or 32 (BVH4) floats per interior node
-  std::vector<float> tris;        // tri_floats per leaf-ordered triangle record (padding records: prim ~0u)
+  std::vector<float> tris;        // 12 floats per leaf-ordered triangle
   int32_t root = 0;
   uint32_t num_nodes = 0;
   uint32_t num_leaves = 0;
@@ -45,8 +43,6 @@ struct BvhResult {
   uint32_t max_stack = 0;         // traversal stack entries needed (push all hit children but one)
   uint32_t wide_depth = 0;        // interior levels of the emitted tree
   double sah_cost = 0.0;
-  uint32_t tri_floats = 12;       // floats per record (12 or 16)
-  uint32_t tri_records = 0;       // records, padding included (== triangles for 12-float records)
 };
 
 // positions: 3 floats per vertex at `stride_bytes` stride (24 for RefVertex).

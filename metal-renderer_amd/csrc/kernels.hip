@@ -282,19 +282,18 @@ __host__ __device__ constexpr uint32_t node_stride_f4(int mode, uint32_t node_f4
 // (node_f4 = float4s per BVH4 node: 8; nodes / tri_records include the
 // occluder tree's, prims are the scene's triangles)
 __host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t node_f4, uint32_t nodes, uint32_t lds_nodes,
-                                                      uint32_t tri_f4, uint32_t tri_records, uint32_t prims,
-                                                      uint32_t mats, uint32_t lights) {
-  if (mode == kAllLds)
-    return node_stride_f4(mode, node_f4) * nodes + tri_f4 * tri_records + 6 * prims + 2 * mats + 7 * lights;
+                                                      uint32_t tri_records, uint32_t prims, uint32_t mats,
+                                                      uint32_t lights) {
+  if (mode == kAllLds) return node_stride_f4(mode, node_f4) * nodes + 3 * tri_records + 6 * prims + 2 * mats + 7 * lights;
   if (mode == kTopLds) return node_f4 * lds_nodes;
   return 0;
 }
 // both trees' nodes and leaf-triangle records (mrt_layout.h DeviceScene)
 __host__ __device__ inline uint32_t scene_nodes(const DeviceScene& sc) { return sc.num_nodes + sc.occ_nodes; }
-__host__ __device__ inline uint32_t scene_tri_records(const DeviceScene& sc) { return sc.tri_records; }
+__host__ __device__ inline uint32_t scene_tri_records(const DeviceScene& sc) { return sc.num_triangles + sc.occ_tris; }
 __host__ __device__ inline uint32_t lds_scene_float4s(int mode, const DeviceScene& sc) {
-  return lds_scene_float4s(mode, node_float4s(sc.width), scene_nodes(sc), sc.lds_nodes, sc.tri_f4,
-                           scene_tri_records(sc), sc.num_triangles, sc.num_materials, sc.num_lights + 1);
+  return lds_scene_float4s(mode, node_float4s(sc.width), scene_nodes(sc), sc.lds_nodes, scene_tri_records(sc),
+                           sc.num_triangles, sc.num_materials, sc.num_lights + 1);
 }
 
 template <int MODE>
@@ -335,11 +334,11 @@ template <int MODE>
 __device__ __forceinline__ void fetch_tri(const DeviceScene& sc, const LdsCtx& cx, uint32_t k, float4& t0,
                                           float4& t1, float4& t2) {
   if (MODE == kAllLds) {
-    t0 = g_lds[cx.tri_base + sc.tri_f4 * k];
-    t1 = g_lds[cx.tri_base + sc.tri_f4 * k + 1];
-    t2 = g_lds[cx.tri_base + sc.tri_f4 * k + 2];
+    t0 = g_lds[cx.tri_base + 3 * k];
+    t1 = g_lds[cx.tri_base + 3 * k + 1];
+    t2 = g_lds[cx.tri_base + 3 * k + 2];
   } else {
-    const float4* p = reinterpret_cast<const float4*>(sc.tris) + sc.tri_f4 * (size_t)k;
+    const float4* p = reinterpret_cast<const float4*>(sc.tris) + 3 * (size_t)k;
     t0 = p[0];
     t1 = p[1];
     t2 = p[2];
@@ -401,7 +400,7 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   const uint32_t node_f4 = node_stride_f4(MODE, nf4);
   const bool copies = node_f4 != nf4;
   cx.tri_base = node_f4 * n_nodes;
-  cx.prim_base = cx.tri_base + sc.tri_f4 * TR;
+  cx.prim_base = cx.tri_base + 3 * TR;
   cx.mat_base = cx.prim_base + 6 * T;
   cx.light_base = cx.mat_base + 2 * M;
   const uint32_t f4 = cx.light_base + 7 * NL;
@@ -414,7 +413,7 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
                             reinterpret_cast<const float4*>(sc.prims), reinterpret_cast<const float4*>(sc.materials),
                             reinterpret_cast<const float4*>(sc.lights)};
     const uint32_t base[5] = {0u, cx.tri_base, cx.prim_base, cx.mat_base, cx.light_base};
-    const uint32_t len[5] = {nf4 * n_nodes, sc.tri_f4 * TR, 6 * T, 2 * M, 7 * NL};
+    const uint32_t len[5] = {nf4 * n_nodes, 3 * TR, 6 * T, 2 * M, 7 * NL};
     for (int r = copies ? 1 : 0; r < 5; ++r)
       for (uint32_t i = threadIdx.x; i < len[r]; i += kBlock) g_lds[base[r] + i] = src[r][i];
     if (copies) {   // quadrant copies: x, y rows (near, far), z rows (lo, hi), refs

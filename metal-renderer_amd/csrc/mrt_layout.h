@@ -84,8 +84,7 @@ constexpr uint32_t kIntersectSpillGrid = 1024;      // persistent grid of the st
 // 4 floats per record.
 struct DeviceScene {
   const float* nodes;        // float4 x 8 per BVH4 node (see above)
-  const float* tris;         // float4 x tri_f4 per leaf-ordered triangle record: (v0, bits(prim)), (e1, 0), (e2, 0)
-                             //   [, (0) for 64-B records]; padding records carry prim ~0u and are never referenced
+  const float* tris;         // float4 x 3 per leaf-ordered triangle: (v0, bits(prim)), (e1, 0), (e2, 0)
   const float* prims;        // float4 x 6 per primitive (original order):
                              //   (p0, bits(material)), (p1, bits(light index or ~0u)), (p2, 0),
                              //   (n0, 0), (n1, 0), (n2, 0)
@@ -101,8 +100,6 @@ struct DeviceScene {
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
   uint32_t width;            // node width: 4 (BVH4; the only layout the kernels traverse)
   uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack; both trees)
-  uint32_t tri_f4;           // float4s per triangle record: 3 (48 B) or 4 (64 B, pairs line-aligned)
-  uint32_t tri_records;      // records of both trees' leaf arrays (LDS staging of whole scenes)
   // shadow-ray occluder tree (occluders.h): the BVH4 over the triangles that
   // are not in a culled plane, stored after the main tree — its nodes are
   // nodes [num_nodes, num_nodes + occ_nodes), its leaf triangles follow the

@@ -56,8 +56,8 @@ bool overlaps(const double (*p)[2], const Rect& r, double m) {
 
 }  // namespace
 
-bool build_primary_lists(const float* tris, uint32_t tri_floats, uint32_t num_tris, uint32_t W, uint32_t H,
-                         uint32_t cap, PrimaryLists& out) {
+bool build_primary_lists(const float* tris, uint32_t num_tris, uint32_t W, uint32_t H, uint32_t cap,
+                         PrimaryLists& out) {
   out = PrimaryLists{};
   if (W < 2 || H < 2 || num_tris == 0 || cap == 0 || cap >= kPrimaryFallback) return false;
   const uint32_t BX = (W + kPrimaryBlock - 1) / kPrimaryBlock, BY = (H + kPrimaryBlock - 1) / kPrimaryBlock;
@@ -78,10 +78,7 @@ bool build_primary_lists(const float* tris, uint32_t tri_floats, uint32_t num_tr
   uint64_t entries = 0;
   const uint64_t budget = nblocks * (uint64_t)cap * 2;   // candidate entries worth building at all
   for (uint32_t k = 0; k < num_tris; ++k) {
-    const float* t = tris + tri_floats * (size_t)k;
-    uint32_t prim_bits;
-    std::memcpy(&prim_bits, &t[3], 4);
-    if (prim_bits == 0xFFFFFFFFu) continue;   // padding record
+    const float* t = tris + 12 * (size_t)k;
     const D3 v0 = {t[0], t[1], t[2]}, e1 = {t[4], t[5], t[6]}, e2 = {t[8], t[9], t[10]};
     const D3 v[3] = {v0, add(v0, e1), add(v0, e2)};
     D3 rel[3];

@@ -30,12 +30,10 @@ struct PrimaryLists {
   double mean_count = 0.0;                  // mean list length over listed blocks
 };
 
-// tris: `tri_floats` (12 or 16) floats per leaf-ordered triangle record
-// {v0, bits(prim), e1, 0, e2, 0[, 0 x 4]}, padding records (prim ~0u) skipped;
-// lists hold record indices.  Lists longer than `cap` fall back to the
-// traversal.  Returns false (and an empty result) when the scene is too
-// dense for lists to pay off.
-bool build_primary_lists(const float* tris, uint32_t tri_floats, uint32_t num_records, uint32_t width,
-                         uint32_t height, uint32_t cap, PrimaryLists& out);
+// tris: 12 floats per leaf-ordered triangle {v0, bits(prim), e1, 0, e2, 0};
+// lists longer than `cap` fall back to the traversal.  Returns false (and an
+// empty result) when the scene is too dense for lists to pay off.
+bool build_primary_lists(const float* tris, uint32_t num_tris, uint32_t width, uint32_t height, uint32_t cap,
+                         PrimaryLists& out);
 
 }  // namespace mrt

@@ -394,7 +394,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
     HIP_TRY(r->primary.alloc(0));
     r->primary_bx = 0;
     if (r->primary_allowed && !r->path_mode &&
-        mrt::build_primary_lists(b.tris.data(), b.tri_floats, b.tri_records, W, H, r->primary_cap, pl)) {
+        mrt::build_primary_lists(b.tris.data(), (uint32_t)(b.tris.size() / 12), W, H, r->primary_cap, pl)) {
       HIP_TRY(upload(r->primary, pl.words.data(), pl.words.size() * 4));
       r->primary_bx = pl.blocks_x;
       r->stats.primary_blocks = pl.listed_blocks;
@@ -719,8 +719,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
   // BVH4 is the one layout the kernels traverse (BVH2 measured -24 %, a
   // compressed BVH8 -33 % and a quantised BVH4 -10 % on C4 in r2)
-  // MRT_TRI64=1: 64-B triangle records (two-triangle leaves in one 128-B line)
-  if (const char* v = std::getenv("MRT_TRI64")) opt.tri_floats = std::atoi(v) ? 16u : 12u;
   opt.width = desc->bvh_width ? desc->bvh_width : 4;
   if (opt.width != 4) return fail(MRT_ERR_INVALID, "bvh_width must be 4 (or 0 = default)");
   if (builder != MRT_BVH_HOST_SAH && builder != MRT_BVH_DEVICE_LBVH && builder != MRT_BVH_DEVICE_PLOC)
@@ -761,8 +759,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     b.width = 4;
     b.max_stack = g.max_stack;
     b.lds_nodes = std::min<uint32_t>(opt.lds_node_budget, g.num_nodes);   // BFS order: any prefix is the top
-    b.tri_floats = 12;   // the device builders write 48-B records
-    b.tri_records = T;
     b.sah_cost = 0.0;
   }
   if (s->bvh.max_stack > (uint32_t)mrt::kMaxTraversalStack)
@@ -820,8 +816,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     occ_on = mrt::find_occluders(h.vertices.data()->v, sizeof(mrt::RefVertex), (uint32_t)h.vertices.size(),
                                  h.indices.data(), T, lv.data(), ln.data(), h.light_count, occ);
   }
-  const uint32_t node_base = (uint32_t)(s->bvh.nodes.size() / 32), tri_base = s->bvh.tri_records;
-  const uint32_t TF = s->bvh.tri_floats;
+  const uint32_t node_base = (uint32_t)(s->bvh.nodes.size() / 32), tri_base = T;
   int32_t occ_root = mrt::kEmptyChild;
   if (occ_on && !occ.keep.empty()) {
     std::vector<uint32_t> sub;
@@ -842,9 +837,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
         float& f = ob.nodes[32 * (size_t)k + 24 + c];
         f = bitsf((uint32_t)rebase((int32_t)fbits(f)));
       }
-    for (size_t i = 0; i < ob.tri_records; ++i) {   // leaf prim ids: subset position -> primitive
-      float& f = ob.tris[TF * i + 3];
-      if (fbits(f) != 0xFFFFFFFFu) f = bitsf(occ.keep[fbits(f)]);   // (padding records stay ~0u)
+    for (size_t i = 0; i < occ.keep.size(); ++i) {   // leaf prim ids: subset position -> primitive
+      float& f = ob.tris[12 * i + 3];
+      f = bitsf(occ.keep[fbits(f)]);
     }
     occ_root = rebase(ob.root);
     // the renderer sizes its LDS stack by the deeper of the two trees
@@ -913,8 +908,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.lds_nodes = s->bvh.lds_nodes;
   d.width = s->bvh.width;
   d.max_stack = s->bvh.max_stack;
-  d.tri_f4 = TF / 4;
-  d.tri_records = (uint32_t)(up_tris.size() / TF);   // both trees' records
   d.occ_root = occ_root;
   d.occ_planes = 0;
   if (occ_on) {
@@ -1035,10 +1028,9 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
   const mrt::HostScene& h = scene->host;
   const uint32_t T = (uint32_t)h.references.size();
   std::vector<uint8_t> all(T, 1);
-  const uint32_t TF = b.tri_floats;
   int rc = check_tree(
-      h, b.root, 0, b.num_nodes, 0, b.tri_records, b.max_stack, all, [&](uint32_t r) { return &b.nodes[32 * (size_t)r]; },
-      [&](uint32_t k) { return &b.tris[TF * (size_t)k]; }, "main tree");
+      h, b.root, 0, b.num_nodes, 0, T, b.max_stack, all, [&](uint32_t r) { return &b.nodes[32 * (size_t)r]; },
+      [&](uint32_t k) { return &b.tris[12 * (size_t)k]; }, "main tree");
   if (rc || scene->occ_keep.empty()) return rc;
   // the occluder tree: exactly the kept primitives, its own stack bound, which
   // the renderer's stack (sized by the deeper tree) covers
@@ -1047,9 +1039,9 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
   const uint32_t occ_nodes = (uint32_t)(scene->occ_nodes.size() / 32);
   if (scene->occ_max_stack > b.max_stack) return fail(MRT_ERR_STATE, "occluder tree: deeper than the main tree");
   return check_tree(
-      h, scene->occ_root, scene->occ_node_base, occ_nodes, b.tri_records, (uint32_t)(scene->occ_tris.size() / TF),
-      scene->occ_max_stack, kept, [&](uint32_t r) { return &scene->occ_nodes[32 * (size_t)(r - scene->occ_node_base)]; },
-      [&](uint32_t k) { return &scene->occ_tris[TF * (size_t)(k - b.tri_records)]; }, "occluder tree");
+      h, scene->occ_root, scene->occ_node_base, occ_nodes, T, (uint32_t)scene->occ_keep.size(), scene->occ_max_stack,
+      kept, [&](uint32_t r) { return &scene->occ_nodes[32 * (size_t)(r - scene->occ_node_base)]; },
+      [&](uint32_t k) { return &scene->occ_tris[12 * (size_t)(k - T)]; }, "occluder tree");
 }
 
 int mrt_scene_destroy(mrt_scene* scene) {
@@ -1123,8 +1115,6 @@ int accel_build(mrt_accel* a) {
   a->dev.nodes = a->nodes.as<float>();
   a->dev.tris = a->tris.as<float>();
   a->dev.num_triangles = T;
-  a->dev.tri_f4 = 3;            // 48-B records (the stage intersect kernel)
-  a->dev.tri_records = T;
   a->dev.width = 4;
   a->dev.lds_nodes = 0;
   a->info.triangles = T;

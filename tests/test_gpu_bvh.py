@@ -199,26 +199,3 @@ def test_device_bvh_deep_scene_matches_sah(gpu, mrt_mod, oracle_mod, builder):
     print(f"builder {builder}: max_stack {scenes[1].info['bvh_max_stack']}, build {scenes[1].info['build_ms']:.1f} ms")
     for sc in scenes:
         sc.close()
-
-
-@pytest.mark.parametrize("precise", [True, False])
-@pytest.mark.parametrize("scene,proc,W,H,L", [("cornellbox", 0, 96, 64, 4), ("CornellBox-Water-plastic", 0, 80, 48, 6),
-                                              ("cornellbox", 65536, 64, 48, 4)])
-def test_tri64_records_render_bitwise(gpu, mrt_mod, monkeypatch, precise, scene, proc, W, H, L):
-    """64-B leaf triangle records (MRT_TRI64=1: two-triangle leaves start at an
-    even record, one 128-B line; padding records are never referenced) give
-    the same images and ray counts as 48-B records, bit for bit, in every
-    kernel the scene runs (stream: cornellbox; path: Water, procedural)."""
-    out = []
-    for tri64 in ("0", "1"):
-        monkeypatch.setenv("MRT_TRI64", tri64)
-        s = mrt_mod.Scene(scene, procedural_triangles=proc)
-        s.check_bvh()
-        r = mrt_mod.Renderer(s, W, H, L, precise=precise)
-        r.draw(2)
-        out.append((r.read_image(), r.stats()["active_ray_bounces"]))
-        r.close()
-        s.close()
-    (a, na), (b, nb) = out
-    assert np.isfinite(a).all() and a[..., :3].max() > 0
-    assert a.tobytes() == b.tobytes() and na == nb

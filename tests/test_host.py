@@ -65,11 +65,9 @@ def test_flatten_matches_oracle(mrt_mod, oracle_mod, scene):
     assert s.info["triangles"] == o.n_triangles and s.info["light_triangles"] == o.n_lights
 
 
-@pytest.mark.parametrize("tri64", ["0", "1"])   # 48-B or 64-B leaf triangle records (MRT_TRI64)
 @pytest.mark.parametrize("scene", SCENES)
 @pytest.mark.parametrize("leaf", [1, 4, 16])
-def test_bvh_structure(mrt_mod, monkeypatch, scene, leaf, tri64):
-    monkeypatch.setenv("MRT_TRI64", tri64)
+def test_bvh_structure(mrt_mod, scene, leaf):
     s = mrt_mod.Scene(scene, device=-1, max_leaf_size=leaf)
     s.check_bvh()   # containment, every primitive once, stack bound
     i = s.info
@@ -86,11 +84,7 @@ def test_bvh_width_default_and_invalid(mrt_mod):
             mrt_mod.Scene("cornellbox", device=-1, bvh_width=w)
 
 
-def test_bvh_procedural_mesh(mrt_mod, monkeypatch):
-    monkeypatch.setenv("MRT_TRI64", "1")   # 64-B records + occluder-free large tree: still a valid structure
-    Scene64 = mrt_mod.Scene("cornellbox", device=-1, procedural_triangles=1 << 16, procedural_seed=3)
-    Scene64.check_bvh()
-    monkeypatch.delenv("MRT_TRI64")
+def test_bvh_procedural_mesh(mrt_mod):
     s = mrt_mod.Scene("cornellbox", device=-1, procedural_triangles=1 << 16, procedural_seed=3, bvh_width=4)
     assert s.info["triangles"] == 36 + (1 << 16)
     s.check_bvh()

@@ -97,7 +97,6 @@ void camera_ray(uint32_t x, uint32_t y, uint32_t W, uint32_t H, float nsx, float
 // block's list; returns violations << 40 | rays
 template <bool F>
 uint64_t check(const BvhResult& b, const PrimaryLists& pl, uint32_t T, uint32_t W, uint32_t H, int jitters) {
-  const uint32_t TF = b.tri_floats;
   std::mt19937 rng(7);
   std::uniform_real_distribution<float> U(0.0f, 1.0f);
   const float extremes[3] = {0.0f, 0.99999994f, 0.5f};   // ns in [0, 1)
@@ -119,10 +118,7 @@ uint64_t check(const BvhResult& b, const PrimaryLists& pl, uint32_t T, uint32_t 
         uint32_t bp = 0xFFFFFFFFu, bk = 0;
         bool found = false;
         for (uint32_t k = 0; k < T; ++k) {
-          const float* t = b.tris.data() + TF * (size_t)k;
-          uint32_t pb;
-          std::memcpy(&pb, &t[3], 4);
-          if (pb == 0xFFFFFFFFu) continue;   // padding record
+          const float* t = b.tris.data() + 12 * (size_t)k;
           float tt;
           if (!tri_bary<F>(o, d, {t[0], t[1], t[2]}, {t[4], t[5], t[6]}, {t[8], t[9], t[10]}, tt)) continue;
           uint32_t prim;
@@ -167,13 +163,12 @@ int main(int argc, char** argv) {
   flatten(sc);
   BvhBuildOptions opt;
   opt.width = 4;
-  if (const char* v = std::getenv("MRT_TRI64")) opt.tri_floats = std::atoi(v) ? 16u : 12u;
   BvhResult b;
   if (!build_bvh(sc.vertices.data()->v, sizeof(RefVertex), sc.indices.data(), (uint32_t)sc.references.size(), opt, b,
                  err)) { std::fprintf(stderr, "%s\n", err.c_str()); return 2; }
-  const uint32_t T = b.tri_records, TF = b.tri_floats;
+  const uint32_t T = (uint32_t)(b.tris.size() / 12);
   PrimaryLists pl;
-  const bool built = build_primary_lists(b.tris.data(), TF, T, W, H, cap, pl);
+  const bool built = build_primary_lists(b.tris.data(), T, W, H, cap, pl);
   if (!built) {
     std::printf("violations 0 blocks %u listed 0 mean 0 (lists not built)\n", (W + 7) / 8 * ((H + 7) / 8));
     return 0;
