@@ -750,7 +750,8 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
 // (tri_bary over the shading record's vertices: the leaf record's v0,
 // e1 = v1 - v0, e2 = v2 - v0 are the same float operations, bvh.cpp) and its
 // acceptance rule, so "occluded" here is the traversal's answer and
-// "not occluded" changes nothing (MRT_ORIGIN_TEST=0 turns it off).
+// "not occluded" changes nothing.  Scenes of >= kOriginTestTriangles only
+// (DeviceScene::origin_test; MRT_ORIGIN_TEST=0 compiles it out).
 #ifndef MRT_ORIGIN_TEST
 #define MRT_ORIGIN_TEST 1
 #endif
@@ -758,6 +759,7 @@ template <int MODE>
 __device__ __forceinline__ bool origin_occludes(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t prim,
                                                 uint32_t target, float tT) {
 #if MRT_ORIGIN_TEST
+  if (!sc.origin_test) return false;   // wave-uniform (kernel argument)
   const V3 p0 = mk(fetch_prim<MODE>(sc, cx, prim, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, prim, 1));
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, prim, 2));
   float t, u, v;
@@ -1957,11 +1959,17 @@ constexpr uint32_t kPathStateWords = 12;
 #ifndef MRT_PATH_WAVES   // 5: 96 VGPRs with 1-3 spilled values (C4 +11 %, C3 +8 % over 4 waves)
 #define MRT_PATH_WAVES 5
 #endif
+// Service threshold: finished nearest queries a wave collects before it
+// shades them together.  With finished shadow queries handled inside the
+// traversal loop (MRT_PATH_INLINE_SHADOW, r4) a service round shades 22 of
+// 64 lanes on C3 instead of 16: C4 2803 -> 2849 Mpaths/s (+1.6 %), C3 2491
+// -> 2601 (+4.4 %) at 24, 2848 / 2620 at 32 (16: 2770 / 2471), alternating
+// in one call.
 #ifndef MRT_PATH_SERVICE
-#define MRT_PATH_SERVICE 24
+#define MRT_PATH_SERVICE 32
 #endif
-#ifndef MRT_PATH_INLINE_SHADOW   // finished shadow queries handled inside the traversal loop (r4)
-#define MRT_PATH_INLINE_SHADOW 0
+#ifndef MRT_PATH_INLINE_SHADOW
+#define MRT_PATH_INLINE_SHADOW 1
 #endif
 
 template <int STACK, int MODE>

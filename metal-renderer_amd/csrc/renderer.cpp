@@ -908,6 +908,8 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.lds_nodes = s->bvh.lds_nodes;
   d.width = s->bvh.width;
   d.max_stack = s->bvh.max_stack;
+  d.origin_test = T >= mrt::kOriginTestTriangles ? 1u : 0u;
+  if (const char* v = std::getenv("MRT_ORIGIN_TEST")) d.origin_test = std::atoi(v) != 0;
   d.occ_root = occ_root;
   d.occ_planes = 0;
   if (occ_on) {
