@@ -23,10 +23,7 @@ namespace mrt {
 // Planes 0-1 are all the traversal needs; planes 2-3 are loaded after the
 // hit so they do not occupy registers during traversal.
 // The bounce index (Ray.params.z) is uniform per launch and not stored.
-// Planes 4-5 exist only for the shadow-queue stream kernel's S levels
-// (kernels.hip stream_sq_kernel): (shadow direction, t of the target light),
-// (light sample L, grazing flag).
-constexpr int kQueuePlanes = 6;
+constexpr int kQueuePlanes = 4;
 struct RayQueue {
   float4* plane[kQueuePlanes];
 };
@@ -62,8 +59,6 @@ constexpr uint32_t kSegSlack = 1024;
 constexpr uint32_t kStreamCap = 128;
 constexpr uint32_t kStreamMaxL = 64;
 inline size_t stream_slots(uint32_t L, uint32_t G) { return (size_t)G * 4 * (L > 1 ? L - 1 : 1) * kStreamCap; }
-// the shadow-queue variant: 2 (L - 1) levels per wave, six planes
-inline size_t stream_sq_slots(uint32_t L, uint32_t G) { return (size_t)G * 4 * (L > 1 ? 2 * (L - 1) : 1) * kStreamCap; }
 
 struct BounceArgs {
   uint32_t width, height;
@@ -151,8 +146,6 @@ constexpr uint32_t kShadeDebugMaterial = 1u;   // BounceArgs::flags / launch_sha
   bool stream_supported(const DeviceScene& sc, uint32_t stack_entries);                                   \
   /* the stream kernel's persistent grid (its LDS has no per-block segment scratch) */                    \
   hipError_t stream_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid);                  \
-  /* ray-queue slots and planes the stream kernel of this build needs (G blocks, L bounces) */            \
-  size_t stream_queue_slots(uint32_t L, uint32_t G, uint32_t* planes);                                  \
   /* the scene's LDS staging mode is not "whole scene in LDS": the path kernel is the faster one */      \
   bool path_preferred(const DeviceScene& sc);                                                             \
   /* accumulateImage over the owned tiles of a batch of frames (in frame order) */                        \

@@ -495,11 +495,14 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 #ifndef MRT_TRAV_LEAF_SLACK   // traverse()'s leaf loop: a lane keeps its untested leaf for the next round
 #define MRT_TRAV_LEAF_SLACK 0
 #endif
+// r4, with the inline shadow finishes (service 32): path slack 8 / 12 / 16
+// C4 2769 / 2852 / 2873, C3 2530 / 2616 / 2660; leaf slack 4 / 8 / 12 C4
+// 2795 / 2852 / 2869, C3 2574 / 2616 / 2638 (one call, alternating)
 #ifndef MRT_PATH_SLACK   // trav_round(): the path kernel
-#define MRT_PATH_SLACK 12
+#define MRT_PATH_SLACK 16
 #endif
 #ifndef MRT_LEAF_SLACK   // trav_round(): the leaf loop's (a kept leaf is tested next round):
-#define MRT_LEAF_SLACK 8 // with path slack 12, C4 2480 -> 2645 (+6.7 %), C3 2340 -> 2474 (+5.7 %);
+#define MRT_LEAF_SLACK 12 // r3, path slack 12: C4 2480 -> 2645 (+6.7 %), C3 2340 -> 2474 (+5.7 %);
 #endif                   // 2 / 4 / 12 / 16 / 24 / 32: C4 2577 / 2605 / 2645 / 2640 / 2623 / 2611
 
 template <int STACK>
@@ -1625,260 +1628,6 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
   span_end(a);
 }
 
-// ---------------------------------------------------------------------------
-// Shadow-queue streaming wavefront (MRT_SHADOW_QUEUE builds, r4 experiment):
-// the NEE shadow query of bounce b no longer runs in the lanes that shaded
-// bounce b (where ~26 % of them have no shadow ray: C2 lane statistics) but
-// as its own queue level, in full 64-ray waves, fused with the same paths'
-// bounce-(b+1) nearest query.  Per wave, level j = 2b (b >= 1) holds rays
-// waiting for their bounce-b nearest query (planes 0-3, as stream_kernel),
-// level j = 2b + 1 the bounce-b shadow ray + the bounce-(b+1) continuation
-// (planes 0-5: P0 (origin, tag), P1 (next direction, target light), P2 (T,
-// pdf), P3 (R, ior), P4 (shadow direction, t_target), P5 (L, graze)).  An
-// iteration of level j: [j odd: the shadow query, lit -> R += L after the
-// reload of P5] -> nearest query of bounce (j + 1) / 2 -> shading -> paths
-// that end: radiance; survivors with a shadow ray that passes the target
-// and origin tests -> level 2b + 1, the others -> level 2b + 2.  The
-// radiance additions keep the reference's order (emission of bounce b, its
-// light sample, emission of bounce b + 1, ...), so the precise build stays
-// bit-identical.  Levels stay below 2 x 64 rays (a level only receives from
-// shallower ones and the deepest full level runs first).
-// ---------------------------------------------------------------------------
-#ifndef MRT_SHADOW_QUEUE
-#define MRT_SHADOW_QUEUE 0
-#endif
-constexpr uint32_t kSqMaxLevels = 2 * (kStreamMaxL - 1);
-
-template <int STACK, int MODE>
-__device__ __forceinline__ void stream_wave_sq(const DeviceScene& sc, const LdsCtx& cx, const BounceArgs& a,
-                                               uint32_t j, bool active, uint32_t idx, uint32_t slot,
-                                               const RayQueue& q, uint32_t outS, uint32_t outB,
-                                               uint64_t lanes_below, uint32_t& wroteS, uint32_t& wroteB) {
-  const bool shadow_level = (j & 1u) != 0;
-  const uint32_t bounce = (j + 1u) >> 1;   // of this iteration's nearest query
-  const bool last = bounce + 1 == a.max_path_length;
-  LS_ADD(14, 1);
-  LS_ADD(15, (uint32_t)__popcll(__ballot(active)));
-  PathState s;
-  uint32_t tag = 0, pblk = 0xFFFFFFFFu;
-  if (active) {
-    if (j == 0) {
-      const uint32_t fj = a.batch == 1u ? 0u : __builtin_amdgcn_readfirstlane(idx / a.num_slots);
-      uint32_t x, y;
-      slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
-      active = (x < a.width) && (y < a.height);
-      if (active) {
-        tag = idx;
-        pblk = (x / kPrimaryBlock) + (y / kPrimaryBlock) * a.primary_bx;
-        const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
-        camera_ray(x, y, a.width, a.height, ns, s.o, s.d);
-      }
-    } else {
-      const float4 q0 = q.plane[0][slot];
-      s.o = mk(q0);
-      tag = fbits(q0.w);
-      s.prevDiffuse = (tag >> 31) ? 1.0f : 0.0f;
-    }
-  }
-  // -- the previous bounce's shadow query (MPS intersect :545-553 +
-  //    lightSamplingHandler :214-231), a full wave of shadow rays
-  bool lit = false;
-  if (shadow_level && active) {
-    const float4 q4 = q.plane[4][slot];   // (shadow direction, t of the target)
-    const uint32_t target = fbits(reinterpret_cast<const float*>(q.plane[1] + slot)[3]);
-    const bool graze = fbits(reinterpret_cast<const float*>(q.plane[5] + slot)[3]) != 0u;
-    if (__ballot(true)) {
-      LS_ADD(16, (uint32_t)__popcll(__ballot(true)));
-      LS_ADD(17, 1);
-    }
-    lit = (a.debug & 1u) || !trace_occluded<STACK, MODE>(sc, cx, s.o, mk(q4), target, q4.w, graze);
-  }
-  if (active && j != 0) {
-    const float* p1 = reinterpret_cast<const float*>(q.plane[1] + slot);
-    s.d = mk(p1[0], p1[1], p1[2]);
-  }
-  // -- nearest hit of the path ray (MPS intersect, Renderer.mm:519-523)
-  Hit h;
-  h.found = false;
-  bool listed = false;
-  if (j == 0 && a.primary) {
-    const uint32_t b0 = __builtin_amdgcn_readfirstlane(pblk);
-    const bool uniform = b0 != 0xFFFFFFFFu && __ballot(active && pblk != b0) == 0;
-    const uint32_t hd = uniform ? __builtin_amdgcn_readfirstlane(a.primary[b0]) : kPrimaryFallback;
-    const uint32_t cnt = hd & 0xFFu;
-    if (cnt != kPrimaryFallback) {
-      listed = true;
-      LS_ADD(18, 1);
-      LS_ADD(19, (uint32_t)__popcll(__ballot(active)));
-      if (active) primary_nearest<MODE>(sc, cx, a.primary + (hd >> 8), cnt, s.o, s.d, h);
-    }
-  }
-  if (active && !listed) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
-  // -- intersectionHandler (Shaders.metal:105-212)
-  const uint32_t gslot = tag & 0x7FFFFFFFu;
-  if (active) {
-    if (j == 0) {
-      s.T = mk(1.0f, 1.0f, 1.0f);
-      s.R = mk(0.0f, 0.0f, 0.0f);
-      s.pdf = 1.0f;
-      s.prevDiffuse = 0.0f;
-      s.ior = 1.00029f;
-    } else {
-      const float4 q2 = q.plane[2][slot], q3 = q.plane[3][slot];
-      s.T = mk(q2);
-      s.pdf = q2.w;
-      s.R = mk(q3);
-      s.ior = q3.w;
-      if (lit) s.R = add(s.R, mk(q.plane[5][slot]));   // the light sample of the previous bounce
-    }
-  }
-  const bool hit_ok = active && h.found && !(h.t < kDistanceEpsilon);
-  ShadowRay sh;
-  sh.valid = false;
-  if (__ballot(hit_ok)) {
-    LS_ADD(12, 1);
-    LS_ADD(13, (uint32_t)__popcll(__ballot(hit_ok)));
-  }
-  if (hit_ok) {
-    const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;
-    uint32_t x, y;
-    slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
-    const uint32_t back = (bounce % 3u) == 0 ? 0u : ((bounce % 3u) == 1 ? 2u : 1u);
-    const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, bounce, a.frame_index + fj)];
-    shade_hit<MODE>(sc, cx, h, s, ns, bounce, a.max_path_length, !last, sh, (a.flags & kShadeDebugMaterial) != 0);
-  }
-  // -- paths that end here go to accumulateImage (:233-249); survivors are
-  //    routed by whether their shadow ray needs an occlusion query
-  if (active && (!hit_ok || last)) a.radiance[gslot] = make_float4(s.R.x, s.R.y, s.R.z, 0.0f);
-  const bool alive = hit_ok && !last;
-  bool need = false;
-  float tT = 0.0f;
-  if (alive && sh.valid) {
-    const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
-    const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
-    float u, v;
-    if (tri_test(sh.o, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
-        !(tT < kDistanceEpsilon)) {
-      if (a.debug & 1u) s.R = add(s.R, sh.L);   // ablation: every shadow ray reaches its target
-      else need = !origin_occludes<MODE>(sc, cx, sh.o, sh.d, h.prim, sh.target, tT);
-    }
-  }
-  const uint64_t mS = __ballot(need), mB = __ballot(alive && !need);
-  const uint32_t tagw = gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u);
-  if (need) {
-    const uint32_t o = outS + (uint32_t)__popcll(mS & lanes_below);
-    q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(tagw));
-    q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, bitsf(sh.target));
-    q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
-    q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
-    q.plane[4][o] = make_float4(sh.d.x, sh.d.y, sh.d.z, tT);
-    q.plane[5][o] = make_float4(sh.L.x, sh.L.y, sh.L.z, bitsf(sh.graze ? 1u : 0u));
-  } else if (alive) {
-    const uint32_t o = outB + (uint32_t)__popcll(mB & lanes_below);
-    q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(tagw));
-    q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
-    q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
-    q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
-  }
-  wroteS = (uint32_t)__popcll(mS);
-  wroteB = (uint32_t)__popcll(mB);
-}
-
-template <int STACK, int MODE>
-__global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_sq_kernel(DeviceScene sc, BounceArgs a) {
-  __shared__ uint32_t s_cnt[kBlock / 64][kSqMaxLevels + 2];   // rays queued per level (wave-private rows)
-  __shared__ uint32_t s_alive[kBlock / 64][kStreamMaxL];      // survivors per bounce (stats)
-  __shared__ uint32_t s_closed;
-  span_begin(a);
-  LS_INIT();
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t L = a.max_path_length;
-  const uint32_t top = L > 1 ? 2 * (L - 1) : 0u;   // deepest level
-  const LdsCtx cx = stage_lds<MODE>(sc, 0, a.stack_spill);
-  for (uint32_t i = lane; i < kSqMaxLevels + 2; i += 64u) s_cnt[wave][i] = 0;
-  for (uint32_t i = lane; i < kStreamMaxL; i += 64u) s_alive[wave][i] = 0;
-  if (tid == 0) s_closed = 0;
-  __syncthreads();
-  uint32_t* cnt = s_cnt[wave];
-  const uint32_t N0 = a.num_slots * a.batch;
-  const uint32_t rlen = ((N0 + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
-  uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
-  const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // this wave's queue: level j (1..top) at slots qbase + (j - 1) * kStreamCap
-  const uint32_t qbase = (blockIdx.x * (kBlock / 64u) + wave) * (top ? top : 1u) * kStreamCap;
-  uint32_t pend = 0, pend_end = 0;
-  bool input = true;
-  for (;;) {
-    uint32_t lvl = 0;
-    for (uint32_t k = top; k >= 1; --k)
-      if (cnt[k] >= 64u) { lvl = k; break; }
-    if (lvl == 0 && input && pend >= pend_end) {
-      uint32_t got = 0xFFFFFFFFu, gend = 0;
-      if (lane == 0) {
-        while (ranges_left) {
-          const uint32_t r0 = cur_range * rlen;
-          if (r0 < N0 && !(__hip_atomic_load(&s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & (1u << cur_range))) {
-            const uint32_t i = atomicAdd(a.grab + cur_range * kGrabStride, kGrab);
-            if (i < rlen && r0 + i < N0) { got = r0 + i; gend = min(N0, min(r0 + rlen, got + kGrab)); break; }
-            atomicOr(&s_closed, 1u << cur_range);
-          }
-          cur_range = cur_range + 1 == kGrabRanges ? 0u : cur_range + 1;
-          --ranges_left;
-        }
-      }
-      got = __builtin_amdgcn_readfirstlane(got);
-      cur_range = __builtin_amdgcn_readfirstlane(cur_range);
-      ranges_left = __builtin_amdgcn_readfirstlane(ranges_left);
-      if (got == 0xFFFFFFFFu) {
-        input = false;
-      } else {
-        pend = got;
-        pend_end = __builtin_amdgcn_readfirstlane(gend);
-      }
-    }
-    uint32_t n, first;
-    bool camera = false;
-    if (lvl == 0 && pend < pend_end) {
-      camera = true;
-      first = pend;
-      n = min(64u, pend_end - pend);
-      pend += n;
-    } else {
-      if (lvl == 0) {
-        for (uint32_t k = top; k >= 1; --k)
-          if (cnt[k] > 0u) { lvl = k; break; }
-        if (lvl == 0) break;
-      }
-      n = min(64u, cnt[lvl]);
-      first = cnt[lvl] - n;
-      cnt[lvl] = first;
-    }
-    const bool active = lane < n;
-    const uint32_t idx = first + lane;
-    const uint32_t slot = qbase + (lvl - 1u) * kStreamCap + first + lane;
-    const uint32_t b = (lvl + 1u) >> 1;   // bounce of this iteration's nearest query
-    const bool more = b + 1 < L;
-    const uint32_t jS = 2 * b + 1, jB = 2 * b + 2;
-    const uint32_t outS = more ? qbase + (jS - 1u) * kStreamCap + cnt[jS] : 0u;
-    const uint32_t outB = more ? qbase + (jB - 1u) * kStreamCap + cnt[jB] : 0u;
-    // the wave reads back rays its own lanes wrote (gfx9 ordering, see stream_kernel)
-    if (!camera) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    LS_ADD(camera ? 26 : 27, 1);
-    uint32_t wS = 0, wB = 0;
-    stream_wave_sq<STACK, MODE>(sc, cx, a, camera ? 0u : lvl, active, idx, slot, a.in_q, outS, outB, lanes_below,
-                                wS, wB);
-    if (more && lane == 0) {
-      cnt[jS] += wS;
-      cnt[jB] += wB;
-      s_alive[wave][b] += wS + wB;
-    }
-  }
-  for (uint32_t bb = lane; bb + 1 < L; bb += 64u)
-    if (s_alive[wave][bb]) atomicAdd(a.bounce_counts + bb, s_alive[wave][bb]);
-  LS_FLUSH();
-  span_end(a);
-}
-
 struct Trav {
   int32_t node, leaf;
   int sp;
@@ -2501,11 +2250,7 @@ hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_e
 // wave-local streaming wavefront: whole-scene-in-LDS scenes, the stack in LDS
 template <int STACK>
 hipError_t launch_stream_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
-#if MRT_SHADOW_QUEUE
-  stream_sq_kernel<STACK, kAllLds><<<dim3(grid), dim3(kBlock), bounce_lds_bytes(sc, kAllLds, STACK, 0), s>>>(sc, a);
-#else
   stream_kernel<STACK, kAllLds><<<dim3(grid), dim3(kBlock), bounce_lds_bytes(sc, kAllLds, STACK, 0), s>>>(sc, a);
-#endif
   return hipGetLastError();
 }
 // the stream kernel's own persistent grid: every block slot its LDS (scene
@@ -2519,13 +2264,8 @@ hipError_t stream_grid_t(const DeviceScene& sc, uint32_t* grid) {
   e = hipGetDeviceProperties(&prop, dev);
   if (e != hipSuccess) return e;
   int occ = 0;
-#if MRT_SHADOW_QUEUE
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, stream_sq_kernel<STACK, kAllLds>, kBlock,
-                                                   bounce_lds_bytes(sc, kAllLds, STACK, 0)) != hipSuccess || occ < 1)
-#else
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, stream_kernel<STACK, kAllLds>, kBlock,
                                                    bounce_lds_bytes(sc, kAllLds, STACK, 0)) != hipSuccess || occ < 1)
-#endif
     occ = 1;
   *grid = (uint32_t)prop.multiProcessorCount * (uint32_t)std::min(occ, 8);
   return hipSuccess;
@@ -2753,16 +2493,6 @@ hipError_t stream_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* 
   if (stack_entries <= 16) return stream_grid_t<16>(sc, grid);
   if (stack_entries <= 24) return stream_grid_t<24>(sc, grid);
   return stream_grid_t<32>(sc, grid);
-}
-
-size_t stream_queue_slots(uint32_t L, uint32_t G, uint32_t* planes) {
-#if MRT_SHADOW_QUEUE
-  *planes = 6;
-  return stream_sq_slots(L, G);
-#else
-  *planes = 4;
-  return stream_slots(L, G);
-#endif
 }
 
 hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t stack_entries, uint32_t grid,

@@ -120,9 +120,11 @@ struct DeviceScene {
 };
 constexpr uint32_t kMaxOccPlanes = 8;
 // the origin-triangle early-out pays where a shadow ray's descent to its own
-// leaf is long: measured C4 (1M triangles) +2.6 %, C3 (7 K) -1.2 %, C2 (36,
-// whole scene in LDS) -1 to -4 % (r4, alternating A/B in one call)
-constexpr uint32_t kOriginTestTriangles = 65536;
+// leaf goes through global memory: measured C4 (1M triangles) +2.6 %, C3
+// (7 K) +0.5 % (with the path kernel's inline shadow finishes), C2 (36, the
+// whole scene in LDS) 9747 / 9755 with it vs 9597 / 9859 and 9860 x 4
+// without (r4, alternating A/B in one call)
+constexpr uint32_t kOriginTestTriangles = 4096;
 
 // camera-ray candidate lists (primary.h): header (offset << 8) | count per
 // 8x8 pixel block; count kPrimaryFallback = traverse the BVH

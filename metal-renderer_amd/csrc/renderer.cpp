@@ -359,18 +359,10 @@ int alloc_frame_buffers(mrt_renderer* r) {
     HIP_TRY(hipMemsetAsync(fs.segments.p, 0, fs.segments.bytes, r->stream));
     // the path kernel keeps the path state in LDS: no ray queues; the
     // streaming wavefront needs only its per-wave queues
-    // (the stream kernel's queue shape is the loaded build's: 4 or 6 planes)
-    uint32_t planes = 4, planes_p = 4;
-    size_t qslots = slots;
-    if (r->stream_mode) {
-      qslots = std::max(mrt::fast::stream_queue_slots(r->desc.max_path_length, r->grid, &planes),
-                        mrt::precise::stream_queue_slots(r->desc.max_path_length, r->grid, &planes_p));
-      planes = std::max(planes, planes_p);
-    }
+    const size_t qslots = r->stream_mode ? mrt::stream_slots(r->desc.max_path_length, r->grid) : slots;
     for (int q = 0; q < 2; ++q)
       for (int p = 0; p < mrt::kQueuePlanes; ++p)
-        HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (r->stream_mode && q == 1) || (uint32_t)p >= planes ? 0
-                                                                                                      : qslots * 16));
+        HIP_TRY(fs.queue[q][p].alloc(r->path_mode || (r->stream_mode && q == 1) ? 0 : qslots * 16));
     HIP_TRY(fs.radiance.alloc(owned_slots * r->batch * 16));
     const uint32_t need = r->scene->dev.max_stack;
     // spill rows of max_stack words per lane (kernels.hip LdsCtx::spill_lane)
@@ -908,7 +900,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.lds_nodes = s->bvh.lds_nodes;
   d.width = s->bvh.width;
   d.max_stack = s->bvh.max_stack;
-  d.origin_test = T >= mrt::kOriginTestTriangles ? 1u : 0u;
+  d.origin_test = T >= mrt::kOriginTestTriangles ? 1u : 0u;   // (global-memory trees)
   if (const char* v = std::getenv("MRT_ORIGIN_TEST")) d.origin_test = std::atoi(v) != 0;
   d.occ_root = occ_root;
   d.occ_planes = 0;
