@@ -164,6 +164,22 @@ struct Hit {
 #ifndef MRT_PUSH3
 #define MRT_PUSH3 0
 #endif
+// MRT_SPILL_FAST: LDS + spill stacks take plain LDS pushes / pops in steps
+// where no lane can reach the spill area (interior_step)
+#ifndef MRT_SPILL_FAST
+#define MRT_SPILL_FAST 1
+#endif
+#ifndef MRT_BUFFER_PRIMS     // shading records through buffer loads too (< 4 GiB: ~44 M triangles)
+#define MRT_BUFFER_PRIMS 0
+#endif
+#ifndef MRT_SPILL_POP_FAST   // the same for the pops outside interior_step (leaf parking, leaf loop)
+#define MRT_SPILL_POP_FAST 0
+#endif
+// MRT_BUFFER_NODES: global-memory nodes fetched with buffer loads (32-bit
+// offsets from one descriptor: no 64-bit address arithmetic per row)
+#ifndef MRT_BUFFER_NODES
+#define MRT_BUFFER_NODES 1
+#endif
 constexpr uint32_t kQuadCopies = 4;                      // (x, y) sign quadrants
 constexpr uint32_t kQuadCopyF4 = 7;                      // six plane rows + the refs row
 constexpr uint32_t kQuadNodeF4 = kQuadCopies * kQuadCopyF4;
@@ -296,6 +312,17 @@ __host__ __device__ inline uint32_t lds_scene_float4s(int mode, const DeviceScen
                            sc.num_triangles, sc.num_materials, sc.num_lights + 1);
 }
 
+// 16-B buffer load at a 32-bit byte offset from a wave-uniform descriptor
+// (no 64-bit address arithmetic per access); the host keeps every buffer
+// read this way below 4 GiB (mrt_scene_create)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0xFFFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  return make_float4(bitsf(v[0]), bitsf(v[1]), bitsf(v[2]), bitsf(v[3]));
+}
+
 template <int MODE>
 __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx& cx, int32_t node, const RayBox& rb,
                                             float4* q) {
@@ -322,10 +349,20 @@ __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx&
       for (int i = 0; i < 6; ++i) q[i] = g_lds[8 * node + row[i]];
       q[6] = g_lds[8 * node + 6];
     } else {
+#if MRT_BUFFER_NODES
+      // one descriptor over the node array (kernel-argument values: wave-
+      // uniform); per row a 32-bit offset node * 128 + row * 16
+      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(sc.nodes);
+      const uint32_t b = (uint32_t)node << 7;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) q[i] = buf_ld4(rs, b + (row[i] << 4));
+      q[6] = buf_ld4(rs, b + 96u);
+#else
       const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 8 * (size_t)node;
 #pragma unroll
       for (int i = 0; i < 6; ++i) q[i] = p[row[i]];
       q[6] = p[6];
+#endif
     }
   }
 }
@@ -338,17 +375,29 @@ __device__ __forceinline__ void fetch_tri(const DeviceScene& sc, const LdsCtx& c
     t1 = g_lds[cx.tri_base + 3 * k + 1];
     t2 = g_lds[cx.tri_base + 3 * k + 2];
   } else {
+#if MRT_BUFFER_NODES
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(sc.tris);
+    const uint32_t b = k * 48u;
+    t0 = buf_ld4(rs, b);
+    t1 = buf_ld4(rs, b + 16u);
+    t2 = buf_ld4(rs, b + 32u);
+#else
     const float4* p = reinterpret_cast<const float4*>(sc.tris) + 3 * (size_t)k;
     t0 = p[0];
     t1 = p[1];
     t2 = p[2];
+#endif
   }
 }
 
 template <int MODE>
 __device__ __forceinline__ float4 fetch_prim(const DeviceScene& sc, const LdsCtx& cx, uint32_t prim, uint32_t i) {
   if (MODE == kAllLds) return g_lds[cx.prim_base + 6 * prim + i];
+#if MRT_BUFFER_PRIMS
+  return buf_ld4(buf_rsrc(sc.prims), prim * 96u + i * 16u);
+#else
   return reinterpret_cast<const float4*>(sc.prims)[6 * (size_t)prim + i];
+#endif
 }
 template <int MODE>
 __device__ __forceinline__ float4 fetch_mat(const DeviceScene& sc, const LdsCtx& cx, uint32_t m, uint32_t i) {
@@ -507,6 +556,15 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 
 template <int STACK>
 __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
+#if MRT_SPILL_POP_FAST
+  // LDS + spill stacks: a plain LDS pop when no active lane's top entry is
+  // in the spill area (wave-uniform test)
+  if (STACK < 0 && !__any(sp > (STACK < 0 ? -STACK : STACK))) {
+    const int32_t n = sp > 0 ? (int32_t)lds_u32()[cx.stack_base + threadIdx.x + (sp - 1) * kBlock] : kDone;
+    sp = max(sp - 1, 0);
+    return n;
+  }
+#endif
   const int32_t n = sp > 0 ? stack_get<STACK>(cx, sp - 1) : kDone;
   sp = max(sp - 1, 0);
   return n;
@@ -552,6 +610,27 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
       MRT_CE(0, 1) MRT_CE(0, 2) MRT_CE(0, 3)
     }
 #undef MRT_CE
+#if MRT_SPILL_FAST
+    // LDS + spill stacks (deep trees): when no lane of the wave can reach
+    // the spill area in this step (sp + 3 <= LDS entries, wave-uniform),
+    // the pushes and the pop are plain LDS accesses — no per-entry
+    // LDS-or-spill branches (their exec-mask bookkeeping was ~40 of the ~250
+    // instructions of a global-tree interior step)
+    if (STACK < 0 && !__any(sp + 3 > (STACK < 0 ? -STACK : STACK))) {
+      constexpr int kL = STACK < 0 ? -STACK : STACK;
+      uint32_t* st = lds_u32() + cx.stack_base + threadIdx.x;
+      if (t[3] < inf) { st[sp * kBlock] = (uint32_t)r[3]; ++sp; }
+      if (t[2] < inf) { st[sp * kBlock] = (uint32_t)r[2]; ++sp; }
+      if (t[1] < inf) { st[sp * kBlock] = (uint32_t)r[1]; ++sp; }
+      int32_t next = r[0];
+      if (!(t[0] < inf)) {
+        next = sp > 0 ? (int32_t)st[(sp - 1) * kBlock] : kDone;
+        sp = max(sp - 1, 0);
+      }
+      (void)kL;
+      return next;
+    }
+#endif
 #if MRT_PUSH3
     if (MODE != kAllLds) {
       // the hit children after the nearest, far to near, as one block of

@@ -878,6 +878,12 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     *out = s.release();
     return MRT_OK;
   }
+  // the kernels address nodes and leaf triangles with 32-bit buffer offsets
+  // (kernels.hip buf_ld4): each array below 4 GiB (~33 M nodes, ~89 M
+  // triangles; a scene beyond that needs the flat-address build)
+  if ((uint64_t)up_nodes.size() * 4 >= (1ull << 32) || (uint64_t)up_tris.size() * 4 >= (1ull << 32) ||
+      (uint64_t)s->bvh.nodes.size() * 4 >= (1ull << 32) || (uint64_t)T * 48 >= (1ull << 32))
+    return fail(MRT_ERR_INVALID, "scene too large: BVH nodes or leaf triangles exceed 4 GiB");
   HIP_TRY(hipSetDevice(desc->device));
   if (builder == MRT_BVH_HOST_SAH) {
     HIP_TRY(upload(s->nodes, up_nodes.data(), up_nodes.size() * 4));
@@ -1105,6 +1111,8 @@ int accel_build(mrt_accel* a) {
     a->info.bvh_max_stack = b.max_stack;
   }
   if (a->dev.max_stack > (uint32_t)mrt::kMaxTraversalStack) return fail(MRT_ERR_INVALID, "BVH needs a deeper traversal stack");
+  if ((uint64_t)a->nodes.bytes >= (1ull << 32) || (uint64_t)a->tris.bytes >= (1ull << 32))   // 32-bit buffer offsets
+    return fail(MRT_ERR_INVALID, "acceleration structure too large: nodes or leaf triangles exceed 4 GiB");
   HIP_TRY(alloc_isect_spill(a->isect_spill, a->dev.max_stack));
   a->dev.nodes = a->nodes.as<float>();
   a->dev.tris = a->tris.as<float>();
