@@ -453,7 +453,8 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
           for (int a = 0; a < 3; ++a) { o[8 * a + c] = lo[a]; o[8 * a + 4 + c] = hi[a]; }
           o[24 + c] = bitsf((uint32_t)child_ref(wide_children[k][c]));
         } else {
-          for (int a = 0; a < 3; ++a) { o[8 * a + c] = 0.0f; o[8 * a + 4 + c] = 0.0f; }
+          // an inverted box: no ray order's slab test hits it (kernels.hip box4)
+          for (int a = 0; a < 3; ++a) { o[8 * a + c] = INFINITY; o[8 * a + 4 + c] = -INFINITY; }
           o[24 + c] = bitsf((uint32_t)kEmptyChild);
         }
       }

@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kB) void k_collapse_level(LevelArgs a) {
   atomicMax(&a.stats[1], child_need);
   for (int c = 0; c < 4; ++c) {
     if (c >= n) {
-      for (int k = 0; k < 3; ++k) { o[8 * k + c] = 0.0f; o[8 * k + 4 + c] = 0.0f; }
+      for (int k = 0; k < 3; ++k) { o[8 * k + c] = __builtin_inff(); o[8 * k + 4 + c] = -__builtin_inff(); }   // inverted box
       o[24 + c] = __uint_as_float((uint32_t)kEmptyChild);
       continue;
     }
@@ -436,9 +436,10 @@ hipError_t build_bvh_gpu(const float* positions, uint32_t stride_bytes, const ui
     if (T) GB_TRY(hipMemcpyAsync(lb.data(), lbox.p, (size_t)T * 32, hipMemcpyDeviceToHost, s));
     GB_TRY(hipStreamSynchronize(s));
     std::vector<float> node(32, 0.0f);
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < 4; ++c) {   // empty slots: kEmptyChild with an inverted box (kernels.hip box4)
       uint32_t ref = (uint32_t)kEmptyChild;
       std::memcpy(&node[24 + c], &ref, 4);
+      for (int k = 0; k < 3; ++k) { node[8 * k + c] = INFINITY; node[8 * k + 4 + c] = -INFINITY; }
     }
     if (T) {
       float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};

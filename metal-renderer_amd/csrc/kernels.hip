@@ -172,6 +172,9 @@ struct Hit {
 #ifndef MRT_BUFFER_PRIMS     // shading records through buffer loads too (< 4 GiB: ~44 M triangles)
 #define MRT_BUFFER_PRIMS 0
 #endif
+#ifndef MRT_EMPTY_BOX   // top-nodes mode: empty child slots masked by their inverted box alone (box4 LIVE)
+#define MRT_EMPTY_BOX 0
+#endif
 #ifndef MRT_SPILL_POP_FAST   // the same for the pops outside interior_step (leaf parking, leaf loop)
 #define MRT_SPILL_POP_FAST 0
 #endif
@@ -223,7 +226,11 @@ __device__ __forceinline__ float slab(float p, float o, float inv, float oinv) {
 // mrt_layout.h); returns each child's entry distance, +inf for a miss or an
 // empty slot.  ORDERED: the x and y plane rows arrive as (near, far) (a
 // quadrant copy, see MRT_NODE_PERM); otherwise as (lo, hi).
-template <int ORDERED>   // 0: (lo, hi) rows; 2: x, y rows (near, far); 3: all rows (near, far)
+// LIVE = false (rows in ray order only): empty child slots are not masked by
+// their ref but by their box — the builders store an inverted box (lo = +inf,
+// hi = -inf) in every empty slot, whose near slab is +inf in every ray order
+// (in the (lo, hi) order min/max would turn it into an infinite box)
+template <int ORDERED, bool LIVE = true>   // 0: (lo, hi) rows; 2: x, y rows (near, far); 3: all rows (near, far)
 __device__ __forceinline__ void box4(const float4* q, V3 o, const RayBox& rb, float tmin, float tmax, float tn[4]) {
 #if MRT_PRECISE
   const float ox = o.x, oy = o.y, oz = o.z;
@@ -250,8 +257,13 @@ __device__ __forceinline__ void box4(const float4* q, V3 o, const RayBox& rb, fl
       tnear = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));
       tfar = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmax));
     }
-    const bool live = (int32_t)fbits(f[24 + k]) != kEmptyChild;
-    tn[k] = (live & (tnear <= tfar)) ? tnear : __builtin_inff();
+    if constexpr (LIVE) {
+      const bool live = (int32_t)fbits(f[24 + k]) != kEmptyChild;
+      tn[k] = (live & (tnear <= tfar)) ? tnear : __builtin_inff();
+    } else {
+      static_assert(ORDERED == 3, "inverted empty boxes miss only with rows in ray order");
+      tn[k] = (tnear <= tfar) ? tnear : __builtin_inff();
+    }
   }
 }
 
@@ -581,7 +593,8 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     {
       float4 q[7];
       fetch_node4<MODE>(sc, cx, node, rb, q);
-      box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0)>(q, o, rb, tmin, tmax, t);
+      box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0),
+           !(MRT_EMPTY_BOX && MRT_ROWSEL && MODE == kTopLds)>(q, o, rb, tmin, tmax, t);
       r[0] = (int32_t)fbits(q[6].x); r[1] = (int32_t)fbits(q[6].y); r[2] = (int32_t)fbits(q[6].z); r[3] = (int32_t)fbits(q[6].w);
     }
     const float inf = __builtin_inff();

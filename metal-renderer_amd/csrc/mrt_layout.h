@@ -68,8 +68,9 @@ static_assert(sizeof(RefLightTriangle) == 100, "RefLightTriangle");
 // one 16-B load yields one box component for all four children:
 //   [0] = lo.x[0..3]  [1] = hi.x[0..3]  [2] = lo.y[0..3]  [3] = hi.y[0..3]
 //   [4] = lo.z[0..3]  [5] = hi.z[0..3]  [6] = bits(ref[0..3])  [7] = 0
-// Unused child slots carry ref == kEmptyChild (and a zero box); the traversal
-// masks them by ref, never by box.
+// Unused child slots carry ref == kEmptyChild and an inverted box (lo = +inf,
+// hi = -inf), which no slab test with the rows in ray order hits; traversals
+// with rows in (lo, hi) order mask them by ref.
 
 constexpr int32_t kEmptyChild = 0x7FFFFFFF;
 constexpr int kLeafCountBits = 4;
