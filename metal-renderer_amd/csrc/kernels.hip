@@ -165,18 +165,20 @@ struct Hit {
 #define MRT_PUSH3 0
 #endif
 // MRT_SPILL_FAST: LDS + spill stacks take plain LDS pushes / pops in steps
-// where no lane can reach the spill area (interior_step)
+// where no lane can reach the spill area (interior_step).  With
+// MRT_BUFFER_NODES: C4 2890 -> 2946 Mpaths/s, C3 2686 -> 2735, C5 1/8 share
+// 1729 -> 1765 (each alone about half of that; r4, alternating in one call)
 #ifndef MRT_SPILL_FAST
 #define MRT_SPILL_FAST 1
 #endif
-#ifndef MRT_BUFFER_PRIMS     // shading records through buffer loads too (< 4 GiB: ~44 M triangles)
-#define MRT_BUFFER_PRIMS 0
-#endif
+// r4 path-kernel instruction diet (A/B in one call, twice each; C4 / C3
+// Mpaths/s): without the two below 2922 / 2752; EMPTY_BOX 3007-3033 /
+// 2818-2823; SPILL_POP_FAST 2971-2976 / 2791-2792
 #ifndef MRT_EMPTY_BOX   // top-nodes mode: empty child slots masked by their inverted box alone (box4 LIVE)
-#define MRT_EMPTY_BOX 0
+#define MRT_EMPTY_BOX 1
 #endif
 #ifndef MRT_SPILL_POP_FAST   // the same for the pops outside interior_step (leaf parking, leaf loop)
-#define MRT_SPILL_POP_FAST 0
+#define MRT_SPILL_POP_FAST 1
 #endif
 // MRT_BUFFER_NODES: global-memory nodes fetched with buffer loads (32-bit
 // offsets from one descriptor: no 64-bit address arithmetic per row)
@@ -405,11 +407,8 @@ __device__ __forceinline__ void fetch_tri(const DeviceScene& sc, const LdsCtx& c
 template <int MODE>
 __device__ __forceinline__ float4 fetch_prim(const DeviceScene& sc, const LdsCtx& cx, uint32_t prim, uint32_t i) {
   if (MODE == kAllLds) return g_lds[cx.prim_base + 6 * prim + i];
-#if MRT_BUFFER_PRIMS
-  return buf_ld4(buf_rsrc(sc.prims), prim * 96u + i * 16u);
-#else
+  // (buffer loads here measured C4 -4 %, C3 -4.5 %: the shading records stay flat loads)
   return reinterpret_cast<const float4*>(sc.prims)[6 * (size_t)prim + i];
-#endif
 }
 template <int MODE>
 __device__ __forceinline__ float4 fetch_mat(const DeviceScene& sc, const LdsCtx& cx, uint32_t m, uint32_t i) {
