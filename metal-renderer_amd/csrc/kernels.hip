@@ -177,6 +177,12 @@ struct Hit {
 #ifndef MRT_EMPTY_BOX   // top-nodes mode: empty child slots masked by their inverted box alone (box4 LIVE)
 #define MRT_EMPTY_BOX 1
 #endif
+#ifndef MRT_PUSH3_FAST   // the spill fast path's pushes as three unconditional LDS writes
+#define MRT_PUSH3_FAST 0
+#endif
+#ifndef MRT_TOP_LDS      // top-nodes mode stages the top BVH nodes in LDS (0: every node from memory)
+#define MRT_TOP_LDS 1
+#endif
 #ifndef MRT_SPILL_POP_FAST   // the same for the pops outside interior_step (leaf parking, leaf loop)
 #define MRT_SPILL_POP_FAST 1
 #endif
@@ -358,7 +364,7 @@ __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx&
     const uint32_t sx = rowsel ? fbits(rb.inv.x) >> 31 : 0u, sy = rowsel ? fbits(rb.inv.y) >> 31 : 0u;
     const uint32_t sz = rowsel ? fbits(rb.inv.z) >> 31 : 0u;
     const uint32_t row[6] = {sx, 1u - sx, 2u + sy, 3u - sy, 4u + sz, 5u - sz};
-    if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
+    if (MODE == kAllLds || (MRT_TOP_LDS && MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
 #pragma unroll
       for (int i = 0; i < 6; ++i) q[i] = g_lds[8 * node + row[i]];
       q[6] = g_lds[8 * node + 6];
@@ -631,9 +637,19 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     if (STACK < 0 && !__any(sp + 3 > (STACK < 0 ? -STACK : STACK))) {
       constexpr int kL = STACK < 0 ? -STACK : STACK;
       uint32_t* st = lds_u32() + cx.stack_base + threadIdx.x;
+#if MRT_PUSH3_FAST
+      // the hit children after the nearest, far to near, as three
+      // unconditional writes (entries above the new top are garbage)
+      const int c = (int)(t[1] < inf) + (int)(t[2] < inf) + (int)(t[3] < inf);
+      st[sp * kBlock] = (uint32_t)(c == 3 ? r[3] : (c == 2 ? r[2] : r[1]));
+      st[(sp + 1) * kBlock] = (uint32_t)(c == 3 ? r[2] : r[1]);
+      st[(sp + 2) * kBlock] = (uint32_t)r[1];
+      sp += c;
+#else
       if (t[3] < inf) { st[sp * kBlock] = (uint32_t)r[3]; ++sp; }
       if (t[2] < inf) { st[sp * kBlock] = (uint32_t)r[2]; ++sp; }
       if (t[1] < inf) { st[sp * kBlock] = (uint32_t)r[1]; ++sp; }
+#endif
       int32_t next = r[0];
       if (!(t[0] < inf)) {
         next = sp > 0 ? (int32_t)st[(sp - 1) * kBlock] : kDone;
@@ -879,6 +895,46 @@ __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V
   if (!(tT >= kDistanceEpsilon)) return false;
   if (origin_occludes<MODE>(sc, cx, o, d, origin, target, tT)) return false;
   return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT, graze);
+}
+
+// Last bounce (bounce + 1 == MAX_PATH_LENGTH): intersectionHandler adds no
+// light sample and makes no next ray there (Shaders.metal:150,199), so the
+// nearest hit matters only if it is an emitter — every emitter is a light
+// triangle (scene flattening) — and only through its emission.  So the
+// nearest query becomes: the nearest (t, prim) over the light triangles
+// alone (leaf-test arithmetic and tie rule over their shading records), then
+// — if one is hit at t >= 1e-4 — the occlusion query "does any other
+// triangle k beat it, (t_k, k) < (t_L, L)" (the shadow query's any-hit
+// traversal).  Not beaten: the nearest hit is that light (emission follows
+// as before); beaten, missed, or nearer than 1e-4: no emission, which is
+// all the reference's nearest hit could add.  Exact (precise build
+// bitwise); scenes with <= kLightShortcutMax light triangles
+// (DeviceScene::light_shortcut), not with DEBUG_MATERIAL (which shades
+// every hit).  Returns true when the occlusion query is still to run (h
+// holds the light hit); false: h.found says whether there is emission.
+template <int MODE>
+__device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, Hit& h) {
+  h.t = __builtin_inff();
+  h.u = h.v = 0.0f;
+  h.prim = 0xFFFFFFFFu;
+  h.found = false;
+  for (uint32_t k = 0; k < sc.num_lights; ++k) {   // wave-uniform
+    const uint32_t prim = fbits(fetch_light<MODE>(sc, cx, k, 3).w);   // lights[k].index
+    const V3 p0 = mk(fetch_prim<MODE>(sc, cx, prim, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, prim, 1));
+    const V3 p2 = mk(fetch_prim<MODE>(sc, cx, prim, 2));
+    float t, u, v;
+    const bool ok = tri_bary(o, d, p0, sub(p1, p0), sub(p2, p0), t, u, v);
+    const bool hit = ok & (t >= 0.0f) & (t <= h.t);
+    if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
+      h.found = true;
+      h.t = t;
+      h.u = u;
+      h.v = v;
+      h.prim = prim;
+    }
+  }
+  if (h.found && h.t < kDistanceEpsilon) h.found = false;   // no emission whatever is nearer
+  return h.found;
 }
 
 // ---------------------------------------------------------------------------
@@ -1377,7 +1433,19 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
       if (active) primary_nearest<MODE>(sc, cx, a.primary + (hd >> 8), cnt, s.o, s.d, h);
     }
   }
-  if (active && !listed) h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+  if (active && !listed) {
+    if (last && sc.light_shortcut && !(a.flags & kShadeDebugMaterial)) {
+      // the last bounce: light triangles, then one occlusion query (last_bounce_light_hit)
+      if (last_bounce_light_hit<MODE>(sc, cx, s.o, s.d, h)) {
+        Hit hh;
+        hh.t = h.t;
+        hh.found = false;
+        if (traverse<STACK, MODE, true>(sc, cx, s.o, s.d, 0.0f, hh, h.prim, sc.root)) h.found = false;
+      }
+    } else {
+      h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
+    }
+  }
   STAMP_AT(st, 1);
   // -- phase 2: intersectionHandler (Shaders.metal:105-212); a miss or a
   //    near hit ends the path (:122-126)
@@ -1812,6 +1880,33 @@ constexpr uint32_t kPathStateWords = 12;
 #define MRT_PATH_INLINE_SHADOW 1
 #endif
 
+// Start the nearest query of `bounce` for the lane's ray (ro, rd): phase 1
+// with a full traversal, or on the last bounce with the light shortcut
+// (last_bounce_light_hit) either a finished query at once (no light hit) or
+// phase 3: the occlusion query of the light hit (h keeps it; target = L).
+template <int MODE>
+__device__ __forceinline__ void begin_nearest(const DeviceScene& sc, const LdsCtx& cx, bool last, bool shortcut,
+                                              V3 ro, V3 rd, Hit& h, Trav& tr, uint32_t& phase, uint32_t& target,
+                                              bool& occluded) {
+  if (last && shortcut) {
+    if (last_bounce_light_hit<MODE>(sc, cx, ro, rd, h)) {
+      phase = 3;
+      target = h.prim;
+      occluded = false;
+      trav_begin(sc.root, tr);
+    } else {
+      phase = 1;
+      tr.node = kDone;
+      tr.leaf = 0;
+      tr.sp = 0;
+    }
+    return;
+  }
+  phase = 1;
+  trav_begin(sc.root, tr);
+  h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
+}
+
 template <int STACK, int MODE>
 __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_closed;
@@ -1840,6 +1935,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   h.t = 0.0f; h.u = h.v = 0.0f; h.prim = 0u; h.found = false;
   bool occluded = false;
   uint32_t target = 0;
+  const bool shortcut = sc.light_shortcut && !(a.flags & kShadeDebugMaterial);
 
   for (;;) {
     LS_ADD(25, 1);
@@ -1883,10 +1979,8 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
           ps[3 * kBlock] = 0u; ps[4 * kBlock] = 0u; ps[5 * kBlock] = 0u;
           ps[6 * kBlock] = fbits(1.0f); ps[7 * kBlock] = fbits(1.00029f);
           ps[11 * kBlock] = idx;   // prevDiffuse 0
-          phase = 1;
           bounce = 0;
-          trav_begin(sc.root, tr);
-          h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
+          begin_nearest<MODE>(sc, cx, L == 1, shortcut, ro, rd, h, tr, phase, target, occluded);
         }
       }
       pool_next += take;
@@ -1911,12 +2005,16 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         bounce += 1;
         atomicAdd(&s_count[bounce - 1], 1u);   // stats: rays alive at the start of this bounce
         rd = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
-        phase = 1;
-        trav_begin(sc.root, tr);
-        h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
+        begin_nearest<MODE>(sc, cx, bounce + 1 == L, shortcut, ro, rd, h, tr, phase, target, occluded);
         fin = trav_done(tr);
       }
 #endif
+      // a finished last-bounce occlusion query (phase 3) is the nearest
+      // query's answer: the light hit unless another triangle beat it
+      if (fin && phase == 3) {
+        h.found = !occluded;
+        phase = 1;
+      }
       const uint64_t going = __ballot(phase != 0 && !fin);
       if (!going) break;
       if ((uint32_t)__popcll(__ballot(fin)) >= (exhausted ? 1u : (uint32_t)MRT_PATH_SERVICE)) break;
@@ -1924,7 +2022,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       LS_ADD(23, (uint32_t)__popcll(going));
       if (phase != 0 && !fin) {
         const RayBox rb = make_raybox(ro, rd);
-        trav_round<STACK, MODE>(sc, cx, ro, rd, rb, h, phase == 2, target, occluded, tr);
+        trav_round<STACK, MODE>(sc, cx, ro, rd, rb, h, phase >= 2, target, occluded, tr);
         fin = trav_done(tr);
       }
     }
@@ -2013,9 +2111,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       atomicAdd(&s_count[bounce - 1], 1u);   // stats: rays alive at the start of this bounce
       // ro already holds the next ray's origin (set at shading, unchanged by a shadow query)
       rd = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
-      phase = 1;
-      trav_begin(sc.root, tr);
-      h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
+      begin_nearest<MODE>(sc, cx, bounce + 1 == L, shortcut, ro, rd, h, tr, phase, target, occluded);
     }
   }
   __syncthreads();
@@ -2238,6 +2334,7 @@ size_t path_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack) {
 DeviceScene fit_path_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack) {
   if (mode != kTopLds) return sc;
   DeviceScene f = sc;
+  if (!MRT_TOP_LDS) { f.lds_nodes = 0; return f; }
   const size_t target = 160 * 1024 / MRT_PATH_WAVES - 2048;
   const size_t fixed = path_lds_bytes(sc, kGlobal, stack) + 64 + 256;   // + static (s_count, s_closed)
   const size_t fit = fixed < target ? (target - fixed) / ((size_t)node_float4s(sc.width) * 16) : 0;

@@ -101,6 +101,8 @@ struct DeviceScene {
   uint32_t lds_nodes;        // number of top nodes (BFS order) staged in LDS by the kernels
   uint32_t width;            // node width: 4 (BVH4; the only layout the kernels traverse)
   uint32_t max_stack;        // traversal stack entries a ray can need (<= kMaxTraversalStack; both trees)
+  uint32_t light_shortcut;   // last-bounce nearest queries test the light triangles and then run one
+                             // occlusion query (kernels.hip last_bounce_light_hit): <= kLightShortcutMax lights
   uint32_t origin_test;      // shadow rays test the triangle they leave before traversing (kernels.hip
                              // origin_occludes): on for deep trees (>= kOriginTestTriangles triangles)
   // shadow-ray occluder tree (occluders.h): the BVH4 over the triangles that
@@ -126,6 +128,8 @@ constexpr uint32_t kMaxOccPlanes = 8;
 // whole scene in LDS) 9747 / 9755 with it vs 9597 / 9859 and 9860 x 4
 // without (r4, alternating A/B in one call)
 constexpr uint32_t kOriginTestTriangles = 4096;
+// light triangles tested per last-bounce ray by last_bounce_light_hit
+constexpr uint32_t kLightShortcutMax = 16;
 
 // camera-ray candidate lists (primary.h): header (offset << 8) | count per
 // 8x8 pixel block; count kPrimaryFallback = traverse the BVH
