@@ -912,6 +912,9 @@ __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V
 // (DeviceScene::light_shortcut), not with DEBUG_MATERIAL (which shades
 // every hit).  Returns true when the occlusion query is still to run (h
 // holds the light hit); false: h.found says whether there is emission.
+// Measured (r4, alternating in one call): C2 (stream kernel) 9738 / 9743 ->
+// 10772 / 10778 Mpaths/s (+10.6 %); the path kernel keeps the full query
+// (MRT_PATH_LAST_LIGHT).
 template <int MODE>
 __device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, Hit& h) {
   h.t = __builtin_inff();
@@ -919,9 +922,13 @@ __device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, con
   h.prim = 0xFFFFFFFFu;
   h.found = false;
   for (uint32_t k = 0; k < sc.num_lights; ++k) {   // wave-uniform
-    const uint32_t prim = fbits(fetch_light<MODE>(sc, cx, k, 3).w);   // lights[k].index
-    const V3 p0 = mk(fetch_prim<MODE>(sc, cx, prim, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, prim, 1));
-    const V3 p2 = mk(fetch_prim<MODE>(sc, cx, prim, 2));
+    // the light record's vertices are the primitive's, in its order
+    // (scene flattening, Renderer.mm:394-413): three independent loads, and
+    // v2 - v1, v3 - v1 are the leaf record's e1, e2 bit for bit
+    const float4 LB = fetch_light<MODE>(sc, cx, k, 1), LD = fetch_light<MODE>(sc, cx, k, 3);
+    const float4 LF = fetch_light<MODE>(sc, cx, k, 5);
+    const uint32_t prim = fbits(LD.w);   // lights[k].index
+    const V3 p0 = mk(LB), p1 = mk(LD), p2 = mk(LF);
     float t, u, v;
     const bool ok = tri_bary(o, d, p0, sub(p1, p0), sub(p2, p0), t, u, v);
     const bool hit = ok & (t >= 0.0f) & (t <= h.t);
@@ -1879,6 +1886,9 @@ constexpr uint32_t kPathStateWords = 12;
 #ifndef MRT_PATH_INLINE_SHADOW
 #define MRT_PATH_INLINE_SHADOW 1
 #endif
+#ifndef MRT_PATH_LAST_LIGHT   // the last-bounce light shortcut (last_bounce_light_hit) in the path kernel
+#define MRT_PATH_LAST_LIGHT 0
+#endif
 
 // Start the nearest query of `bounce` for the lane's ray (ro, rd): phase 1
 // with a full traversal, or on the last bounce with the light shortcut
@@ -1935,7 +1945,10 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   h.t = 0.0f; h.u = h.v = 0.0f; h.prim = 0u; h.found = false;
   bool occluded = false;
   uint32_t target = 0;
-  const bool shortcut = sc.light_shortcut && !(a.flags & kShadeDebugMaterial);
+  // (off by default here: the light test's loads inside the traversal loop
+  // and the service cost more than the 11 % of traversal rounds they save —
+  // C4 3056 vs 3096, C3 2783 vs 2880 Mpaths/s with it, r4)
+  const bool shortcut = MRT_PATH_LAST_LIGHT && sc.light_shortcut && !(a.flags & kShadeDebugMaterial);
 
   for (;;) {
     LS_ADD(25, 1);
