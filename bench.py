@@ -354,6 +354,7 @@ def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_
     lane_util = pmc.get("valu_lane_util")
     step_launch_s = step_s / max(1e-9, launches_per_step)     # wall-clock step time per launch
     prof_s = (pmc.get("avg_launch_ns_rocprof_timed") or pmc.get("avg_launch_ns_rocprof") or 0) * 1e-9
+    period_s = (pmc.get("period_ns_rocprof_2streams") or 0) * 1e-9
     roofs = {}
 
     def fracs(per_launch, peak):
@@ -361,6 +362,8 @@ def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_
              "frac_vs_launch": round(per_launch / launch_s / peak, 4)}
         if prof_s:
             f["frac_vs_profile"] = round(per_launch / prof_s / peak, 4)
+        if period_s:
+            f["frac_vs_profile_period"] = round(per_launch / period_s / peak, 4)
         return f
 
     if traffic:
@@ -372,7 +375,7 @@ def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_
         v = {"achieved": round(t, 2), "peak": round(VALU_PEAK_TLANE, 2), "unit": "T VALU lane-slots/s",
              **fracs(valu_insts * 64 / 1e12, VALU_PEAK_TLANE), "wave_instructions_per_launch": valu_insts}
         if lane_util:
-            for k in ("frac", "frac_vs_launch", "frac_vs_profile"):
+            for k in ("frac", "frac_vs_launch", "frac_vs_profile", "frac_vs_profile_period"):
                 if k in v:
                     v["valu_useful_" + k] = round(v[k] * lane_util, 4)
         roofs["valu-issue"] = v
@@ -387,13 +390,16 @@ def roofline(args, pmc_path, whole_frame, timed, launch_s, step_s, launches_per_
     out.update({"bound": bound, "traffic": traffic, "roofs": roofs,
                 "clocks": {"frac": f"wall-clock step time per launch {step_launch_s * 1e3:.4f} ms",
                            "frac_vs_launch": f"this run's per-launch kernel time {launch_s * 1e3:.4f} ms",
-                           "frac_vs_profile": (f"rocprofv3 trace average {prof_s * 1e3:.4f} ms"
-                                               if prof_s else None)},
+                           "frac_vs_profile": (f"rocprofv3 trace average {prof_s * 1e3:.4f} ms (one render "
+                                               f"stream, timed launches)" if prof_s else None),
+                           "frac_vs_profile_period": (f"rocprofv3 trace period {period_s * 1e3:.4f} ms per launch "
+                                                      f"(two render streams)" if period_s else None)},
                 "wait_any_frac": pmc.get("wait_any_frac"),
                 "valu_lane_util": lane_util,
                 "pmc_clock_ghz": pmc.get("clock_ghz"),
                 "rocprof_avg_launch_ms": round(prof_s * 1e3, 4) if prof_s else None,
                 "rocprof_timed_launches": pmc.get("timed_launches_rocprof"),
+                "rocprof_period_ms_2streams": round(period_s * 1e3, 4) if period_s else None,
                 "source": f"profiles/{os.path.basename(pmc_path)} (tag {pmc.get('tag')}, commit "
                           f"{pmc.get('commit', 'unrecorded')}, lib md5 {pmc.get('lib_md5')})",
                 "same_library": (pmc.get("lib_md5") == lib_md5(mrt.LIB_PATH)) if pmc.get("lib_md5") else None})

@@ -23,6 +23,12 @@ BENCH="python3 bench.py --config $CFG --steps $STEPS --warmup $WARM --no-cpu-bas
 set -o pipefail
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1; local rc=$?; tail -n 3 $OUT/$name.log; echo "== $name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -f csv -- $BENCH
+# the same run at the renderer's default two render streams: the trace's
+# period per launch (first start to last end of the timed launches / count)
+# is the kernel's share of the step the bench times
+export MRT_INFLIGHT=2
+step trace2 300 rocprofv3 --kernel-trace -d $OUT/trace2 -o run -f csv -- $BENCH
+export MRT_INFLIGHT=1
 step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/fetch -o run -f csv -- $BENCH
 step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/write -o run -f csv -- $BENCH
 step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/sq -o run -f csv -- $BENCH
