@@ -1982,16 +1982,30 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       LS_ADD(24, (uint32_t)__popcll(__ballot(phase == 0 && rank < take)));
       if (phase == 0 && rank < take) {
         const uint32_t idx = pool_next + rank;
-        const uint32_t fj = a.batch == 1u ? 0u : idx / a.num_slots;
+        // sample index -> (frame fj, slot sl): frame-major, or (sc.region_grabs)
+        // block-major — 8x8 pixel block, then frame, then pixel — so that a
+        // grab range (1/kGrabRanges of the launch) is one band of the image
+        // over all the batch's frames, and the blocks of one XCD (block ids
+        // = x mod 8) start on ranges x and x + 8: their rays meet the same
+        // geometry in that XCD's L2
+        uint32_t fj, sl;
+        if (sc.region_grabs) {
+          const uint32_t q = idx >> 6, blk = q / a.batch;
+          fj = q - blk * a.batch;
+          sl = (blk << 6) | (idx & 63u);
+        } else {
+          fj = a.batch == 1u ? 0u : idx / a.num_slots;
+          sl = idx - fj * a.num_slots;
+        }
         uint32_t x, y;
-        slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+        slot_pixel(sl, a.shard_rank, a.shard_count, a.tiles_x, x, y);
         if ((x < a.width) && (y < a.height)) {
           const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
           camera_ray(x, y, a.width, a.height, ns, ro, rd);
           ps[0 * kBlock] = fbits(1.0f); ps[1 * kBlock] = fbits(1.0f); ps[2 * kBlock] = fbits(1.0f);
           ps[3 * kBlock] = 0u; ps[4 * kBlock] = 0u; ps[5 * kBlock] = 0u;
           ps[6 * kBlock] = fbits(1.0f); ps[7 * kBlock] = fbits(1.00029f);
-          ps[11 * kBlock] = idx;   // prevDiffuse 0
+          ps[11 * kBlock] = fj * a.num_slots + sl;   // the global slot; prevDiffuse 0
           bounce = 0;
           begin_nearest<MODE>(sc, cx, L == 1, shortcut, ro, rd, h, tr, phase, target, occluded);
         }

@@ -105,6 +105,8 @@ struct DeviceScene {
                              // occlusion query (kernels.hip last_bounce_light_hit): <= kLightShortcutMax lights
   uint32_t origin_test;      // shadow rays test the triangle they leave before traversing (kernels.hip
                              // origin_occludes): on for deep trees (>= kOriginTestTriangles triangles)
+  uint32_t region_grabs;     // path kernel: grab ranges are image bands over all frames (kernels.hip
+                             // path_kernel refill): on for deep trees (>= kRegionGrabTriangles)
   // shadow-ray occluder tree (occluders.h): the BVH4 over the triangles that
   // are not in a culled plane, stored after the main tree — its nodes are
   // nodes [num_nodes, num_nodes + occ_nodes), its leaf triangles follow the
@@ -128,6 +130,9 @@ constexpr uint32_t kMaxOccPlanes = 8;
 // whole scene in LDS) 9747 / 9755 with it vs 9597 / 9859 and 9860 x 4
 // without (r4, alternating A/B in one call)
 constexpr uint32_t kOriginTestTriangles = 4096;
+// block-major grab ranges (path kernel): measured (r4, alternating in one
+// call) C4 +1.0 / +0.6 %, C5 1/8 share +0.2 / +0.4 %, C3 (7 K) -2.6 %
+constexpr uint32_t kRegionGrabTriangles = 65536;
 // light triangles tested per last-bounce ray by last_bounce_light_hit
 constexpr uint32_t kLightShortcutMax = 16;
 

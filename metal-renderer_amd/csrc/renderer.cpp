@@ -908,6 +908,8 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.max_stack = s->bvh.max_stack;
   d.origin_test = T >= mrt::kOriginTestTriangles ? 1u : 0u;   // (global-memory trees)
   if (const char* v = std::getenv("MRT_ORIGIN_TEST")) d.origin_test = std::atoi(v) != 0;
+  d.region_grabs = T >= mrt::kRegionGrabTriangles ? 1u : 0u;
+  if (const char* v = std::getenv("MRT_REGIONS")) d.region_grabs = std::atoi(v) != 0;
   d.light_shortcut = h.light_count <= mrt::kLightShortcutMax ? 1u : 0u;
   if (const char* v = std::getenv("MRT_LAST_LIGHT")) d.light_shortcut = d.light_shortcut && std::atoi(v) != 0;
   d.occ_root = occ_root;
