@@ -7,6 +7,7 @@
 #include <cstring>
 #include <array>
 #include <deque>
+#include <functional>
 
 namespace mrt {
 namespace {
@@ -306,13 +307,65 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
   }
   if (!b.err.empty()) { error = b.err; return false; }
   // ---- collapse to the output width ----------------------------------------
-  // A wide node's children are found by repeatedly opening the largest-area
-  // interior child of the binary node (width 2 is the identity).
+  // Greedy: a wide node's children are found by repeatedly opening the
+  // largest-area interior child of the binary node (width 2 is the identity).
+  // DP (opt.collapse_dp, width 4): the binary leaves stay leaves, so the
+  // collapse only chooses which binary interior nodes become wide nodes; the
+  // SAH's expected node visits are the summed area of those.  best[m][k] =
+  // least summed area covering m's subtree with at most k + 1 child slots
+  // (m itself as one slot: area(m) + its own best 4-slot split), computed
+  // bottom-up (children have larger build ids than their parent).
   const std::vector<BuildNode>& bn = b.nodes;
   const uint32_t W = opt.width;
   auto is_leaf = [&](int32_t id) { return bn[id].child[0] < 0; };
+  const bool dp = opt.collapse_dp && W == 4;
+  std::vector<std::array<float, 4>> best;
+  std::vector<std::array<uint8_t, 4>> pick;   // k1 of the split (0: m is one slot)
+  std::vector<uint8_t> inner;                 // m as a wide node: k1 of its children's slots (k2 = 4 - k1 at most)
+  std::vector<uint8_t> inner2;
+  if (dp) {
+    best.assign(bn.size(), {0.0f, 0.0f, 0.0f, 0.0f});
+    pick.assign(bn.size(), {0, 0, 0, 0});
+    inner.assign(bn.size(), 1);
+    inner2.assign(bn.size(), 1);
+    for (size_t i = bn.size(); i-- > 0;) {
+      if (is_leaf((int32_t)i)) continue;   // a leaf costs nothing here, in any number of slots
+      const int32_t l = bn[i].child[0], r = bn[i].child[1];
+      float in = FLT_MAX;
+      for (uint32_t k1 = 1; k1 <= 3; ++k1)
+        for (uint32_t k2 = 1; k1 + k2 <= 4; ++k2) {
+          const float c = best[l][k1 - 1] + best[r][k2 - 1];
+          if (c < in) { in = c; inner[i] = (uint8_t)k1; inner2[i] = (uint8_t)k2; }
+        }
+      best[i][0] = bn[i].box.area() + in;
+      pick[i][0] = 0;
+      for (uint32_t k = 1; k < 4; ++k) {   // at most k + 1 slots
+        best[i][k] = best[i][k - 1];
+        pick[i][k] = pick[i][k - 1];
+        for (uint32_t k1 = 1; k1 <= k; ++k1) {
+          const uint32_t k2 = k + 1 - k1;
+          const float c = best[l][k1 - 1] + best[r][k2 - 1];
+          if (c < best[i][k]) { best[i][k] = c; pick[i][k] = (uint8_t)k1; }
+        }
+      }
+    }
+  }
+  // the children of wide node `id` under the DP choice
+  std::function<void(int32_t, uint32_t, int32_t*, uint32_t&)> expand = [&](int32_t m, uint32_t k, int32_t* ch,
+                                                                             uint32_t& n) {
+    if (is_leaf(m) || pick[m][k - 1] == 0) { ch[n++] = m; return; }
+    const uint32_t k1 = pick[m][k - 1];
+    expand(bn[m].child[0], k1, ch, n);
+    expand(bn[m].child[1], k - k1, ch, n);
+  };
   auto collapse = [&](int32_t id, int32_t ch[4]) {
     uint32_t n = 2;
+    if (dp) {
+      n = 0;
+      expand(bn[id].child[0], inner[id], ch, n);
+      expand(bn[id].child[1], inner2[id], ch, n);
+      return n;
+    }
     ch[0] = bn[id].child[0];
     ch[1] = bn[id].child[1];
     while (n < W) {

@@ -29,6 +29,8 @@ struct BvhBuildOptions {
   bool full_sweep = false;        // exact sweep SAH at every node (presorted, O(n log n)); opt-in (MRT_FULL_SWEEP=1)
   float traversal_cost = 1.0f;    // relative to one triangle test
   uint32_t width = 2;             // 2 = the binary SAH tree itself, 4 = BVH4 (128-B nodes, collapsed; what the kernels traverse)
+  bool collapse_dp = true;        // BVH4: the collapse that minimises the summed area of the wide interior nodes
+                                  // (dynamic programming over the binary tree) instead of greedy largest-area opening
 };
 
 struct BvhResult {
