@@ -9,6 +9,8 @@
   from global memory, traversal stack spilling to global memory) against the
   oracle's brute force over all 1,048,612 triangles, L = 4 (C4) and L = 8
   (C5), precise build;
+* C4 and C5 at full size (1080p L = 4, 4K L = 8), precise build
+  bit-identical to the oracle's CPU BVH;
 * C5's tile sharding: 8 shards of the 4K frame at L = 8 sum bitwise to the
   1-GPU image;
 * C3 and its glass variant C3g (all four BSDFs) at full size, L = 8,
@@ -125,6 +127,26 @@ def test_1m_triangles_match_bruteforce_oracle(big_scene, mrt_mod, L):
           f"A {st['active_ray_bounces']} vs {A}, max_stack {sc.info['bvh_max_stack']}")
     assert np.mean(rel <= 1e-4) >= 0.999 and rmse <= 1e-3
     assert st["active_ray_bounces"] == A
+
+
+@pytest.mark.parametrize("W,H,L,frames", [(1920, 1080, 4, 2), (3840, 2160, 8, 1)], ids=["C4", "C5"])
+def test_1m_triangles_full_size_match_oracle(big_scene, mrt_mod, oracle_mod, W, H, L, frames):
+    """C4 and C5 at FULL size (1080p L = 4; 4K L = 8) through the path
+    megakernel (top nodes in LDS, the rest, the leaves and the stack spill in
+    global memory, block-major grab ranges): precise build bit-identical to
+    the oracle (its CPU BVH over all 1,048,612 triangles: the brute force's
+    answers, tests/test_oracle.py) with the same active ray-bounce count."""
+    sc, osc = big_scene
+    ref, A = osc.render(W, H, L, SEED, frames, threads=host_threads(), flags=oracle_mod.BVH)
+    r = mrt_mod.Renderer(sc, W, H, L, precise=True)
+    r.draw(frames)
+    img, st = r.read_image(), r.stats()
+    r.close()
+    rel, rmse, same = pixel_metrics(img, ref)
+    print(f"1M tris {W}x{H} L={L}: kernel {st['kernel']}, bit-identical {same:.6f}, "
+          f"A {st['active_ray_bounces']} vs {A}")
+    assert st["kernel"] == 1   # the path megakernel
+    assert same == 1.0 and st["active_ray_bounces"] == A
 
 
 def test_c5_shards_sum_to_single_gpu(big_scene, mrt_mod, monkeypatch):
