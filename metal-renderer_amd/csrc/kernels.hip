@@ -558,6 +558,9 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 #ifndef MRT_TRAV_SLACK   // traverse(): stream / bounce / stage kernels
 #define MRT_TRAV_SLACK 0
 #endif
+#ifndef MRT_ZERO_NEE   // shade_hit: no shadow query for a light sample of exactly zero
+#define MRT_ZERO_NEE 1
+#endif
 #ifndef MRT_TRAV_LEAF_SLACK   // traverse()'s leaf loop: a lane keeps its untested leaf for the next round
 #define MRT_TRAV_LEAF_SLACK 0
 #endif
@@ -1145,7 +1148,7 @@ __device__ __forceinline__ uint32_t shade_noise_cell(uint32_t x, uint32_t y, uin
 // renderer/Shaders.metal:128-211.  Emits the NEE shadow ray (when
 // bounce + 1 < L), adds MIS-weighted emission, and — when `next` — samples
 // the next bounce and updates the throughput.
-template <int MODE>
+template <int MODE, bool SKIP_ZERO = (MRT_ZERO_NEE != 0)>
 __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& cx, const Hit& h, PathState& s,
                                           const float4& ns, uint32_t bounce, uint32_t L, bool next, ShadowRay& sh,
                                           bool debug_material) {
@@ -1214,7 +1217,14 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
     sh.o = add(hv, mul(hn, kDistanceEpsilon));
     sh.d = dirToLight;
     sh.target = lindex;
+    // A light sample of exactly zero (a mirror, a plastic mirror lobe or a
+    // dielectric pass-through: the material's BSDF is 0 toward the light)
+    // changes nothing whether or not it is occluded — R + 0 == R bit for bit,
+    // R never being -0 (it starts at +0 and +0 + -0 == +0) — so its shadow
+    // query is not traced (MRT_ZERO_NEE=0, and the B-2 stage kernel, whose
+    // shadow-ray records follow the reference: traced as the reference does)
     sh.valid = (lightPdf > 0.0f) && (lindex != h.prim);
+    if (SKIP_ZERO) sh.valid = sh.valid && !((sh.L.x == 0.0f) & (sh.L.y == 0.0f) & (sh.L.z == 0.0f));
   }
   // emission with MIS — Shaders.metal:180-197 (the light vertex re-derived
   // there is the hit vertex itself: lights[ref.lightTriangleIndex].index == prim)
@@ -2264,7 +2274,7 @@ __global__ __launch_bounds__(kBlock) void shade_kernel(DeviceScene sc, uint32_t 
   h.t = is.distance; h.prim = is.triangleIndex; h.u = is.coordinates[0]; h.v = is.coordinates[1]; h.found = true;
   ShadowRay sh;
   const LdsCtx cx = stage_lds<kGlobal>(sc, 0);
-  shade_hit<kGlobal>(sc, cx, h, s, noise[shade_noise_cell(x, y, bounce, f)], bounce, L, true, sh,
+  shade_hit<kGlobal, false>(sc, cx, h, s, noise[shade_noise_cell(x, y, bounce, f)], bounce, L, true, sh,
                      (flags & kShadeDebugMaterial) != 0);
   if (bounce + 1 < L) {
     sr.origin[0] = sh.o.x; sr.origin[1] = sh.o.y; sr.origin[2] = sh.o.z;
