@@ -118,6 +118,25 @@ def test_full_sweep_sah_builder(mrt_mod, monkeypatch):
     s.close()
 
 
+@pytest.mark.parametrize("scene,proc", [("cornellbox", 0), ("CornellBox-Water-plastic", 0), ("cornellbox", 1 << 15)])
+def test_area_optimal_collapse(mrt_mod, monkeypatch, scene, proc):
+    """The BVH4 collapse by dynamic programming (bvh.cpp, MRT_COLLAPSE=1; the
+    default below 64 K triangles) keeps the binary tree's leaves and picks the
+    wide interior nodes of least summed area: a valid tree (containment, every
+    primitive once, stack bound) whose SAH cost is below the greedy
+    largest-area collapse's (MRT_COLLAPSE=0), with no more nodes."""
+    got = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MRT_COLLAPSE", mode)
+        s = mrt_mod.Scene(scene, device=-1, procedural_triangles=proc)
+        s.check_bvh()
+        got[mode] = (s.info["bvh_sah_cost"], s.info["bvh_nodes"], s.info["bvh_leaves"])
+        s.close()
+    (c0, n0, l0), (c1, n1, l1) = got["0"], got["1"]
+    assert l1 == l0                   # the same binary leaves
+    assert c1 < c0 and n1 <= n0
+
+
 def test_mtl_override_glass_variant(mrt_mod, tmp_path):
     """BASELINE C3 glass variant: Ks 0 0 +1.5 instantiates MATERIAL_SMOOTH_DIELECTRIC."""
     src = open(mrt_mod.scene_path("CornellBox-Water-plastic")[:-4] + ".mtl").read()
