@@ -1788,7 +1788,16 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(Device
     // (stores counted by vscnt) it would need a wavefront-scope
     // release/acquire fence instead (measured within +0.5 % here, DESIGN.md
     // §2.1a).
+#if MRT_LANESTATS
+    // diagnostic: cycles this wait costs the wave (slot 28) over its level iterations (slot 29)
+    uint64_t w0_, w1_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w0_)::"memory");
     if (!camera) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w1_)::"memory");
+    if (!camera) { LS_ADD(28, (uint32_t)(w1_ - w0_)); LS_ADD(29, 1); }
+#else
+    if (!camera) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     LS_ADD(camera ? 26 : 27, 1);
     const uint32_t wrote = bounce_wave<STACK, MODE, true>(sc, cx, a, camera ? 0u : lvl, active, idx, slot,
                                                                  a.in_q, a.in_q, nullptr, out, 0u, lanes_below, st);

@@ -25,7 +25,8 @@ NAMES = ["near_lanes", "near_calls", "near_int_iters", "near_int_lanes", "near_l
          "occ_lanes", "occ_calls", "occ_int_iters", "occ_int_lanes", "occ_leaf_iters", "occ_leaf_lanes",
          "shade_calls", "shade_lanes", "wave_calls", "wave_active", "shadow_rays", "shadow_calls",
          "list_calls", "list_lanes", "svc_rounds", "svc_lanes", "trav_rounds", "trav_lanes", "refill_lanes",
-         "outer_iters", "stream_camera_iters", "stream_level_iters"]
+         "outer_iters", "stream_camera_iters", "stream_level_iters", "stream_queue_wait_cycles",
+         "stream_queue_waits"]
 
 
 def main():
@@ -76,6 +77,10 @@ def main():
         out["shade_util"] = util(c["shade_lanes"], c["shade_calls"])
         out["shadow_phase_util"] = util(c["shadow_rays"], c["shadow_calls"])
         out["list_util"] = util(c["list_lanes"], c["list_calls"])
+        if c.get("stream_queue_waits"):
+            # shader-clock cycles (s_memtime) a wave spends in the queue
+            # iteration's wait for its own stores, per level iteration
+            out["queue_wait_cycles_per_iter"] = round(c["stream_queue_wait_cycles"] / c["stream_queue_waits"], 2)
     print(json.dumps(out))
 
 
