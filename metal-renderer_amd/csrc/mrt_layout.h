@@ -133,6 +133,9 @@ constexpr uint32_t kOriginTestTriangles = 4096;
 // block-major grab ranges (path kernel): measured (r4, alternating in one
 // call) C4 +1.0 / +0.6 %, C5 1/8 share +0.2 / +0.4 %, C3 (7 K) -2.6 %
 constexpr uint32_t kRegionGrabTriangles = 65536;
+// the area-optimal BVH4 collapse (bvh.cpp) below this many triangles, the
+// greedy one above (measured in renderer.cpp mrt_scene_create)
+constexpr uint32_t kGreedyCollapseTriangles = 65536;
 // light triangles tested per last-bounce ray by last_bounce_light_hit
 constexpr uint32_t kLightShortcutMax = 16;
 

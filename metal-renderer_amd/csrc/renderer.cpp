@@ -712,7 +712,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   // triangles: C2 +0.8 %, C3 +1.9 %, C3g +0.5 %; the 1M-triangle C4 tree
   // (21 % fewer, fuller nodes: more children pushed per step) -1.2 %, so it
   // keeps the greedy collapse (r4, alternating in one call)
-  opt.collapse_dp = T < 65536;
+  opt.collapse_dp = T < mrt::kGreedyCollapseTriangles;
   if (const char* v = std::getenv("MRT_COLLAPSE")) opt.collapse_dp = std::atoi(v) != 0;   // 0: greedy, 1: DP
   const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
   // BVH4 is the one layout the kernels traverse (BVH2 measured -24 %, a
