@@ -64,6 +64,13 @@ CONFIGS = {
     # renderer/Renderer.mm:517 loops MAX_PATH_LENGTH, Raytracing.h:23)
     "c2l5": dict(workload="C2 at L=5: cornellbox 1920x1080 64spp, primary ray + 4 bounces (diffuse BSDF)",
                  scene="cornellbox", mtl=None, width=1920, height=1080, spp=64, L=5, procedural=0),
+    # C2 at the reference's own cadence: one drawInMTKView: (1 spp) per call
+    # (renderer/Renderer.mm:587-638) — a step is 64 calls of mrt_renderer_draw,
+    # progressive (no reset between steps, so every step renders new frames and
+    # their noise tables are generated inside the timed region)
+    "c2i": dict(workload="C2 at the per-frame cadence: 64 calls of mrt_renderer_draw (1 spp each) per step, "
+                         "progressive, noise generated inside the timed region", scene="cornellbox", mtl=None,
+                width=1920, height=1080, spp=64, L=4, procedural=0, cadence="frame"),
     # configs[4]: C4's scene at 4K, 256 spp, L = 8 — the 8-GPU configuration
     # (one GPU's share is measured with --shard-of 8)
     "c5": dict(workload="C5 1M-triangle procedural mesh 3840x2160 256spp L=8", scene="cornellbox", mtl=None,
@@ -443,8 +450,10 @@ def main():
                                    "ploc": mrt.BVH_DEVICE_PLOC}[args.bvh])
     r = mrt.Renderer(scene, W, H, L, precise=args.precise, profile=not args.no_kernel_timing,
                      shard_rank=(args.shard_rank if args.shard_of else rank), shard_count=shard_count)
-    r.prepare(spp)
-    prep = r.stats()   # noise window of the step's spp frames, generated + uploaded before the timed region
+    per_frame = cfg.get("cadence") == "frame"
+    if not per_frame:
+        r.prepare(spp)
+    prep = r.stats()   # noise chunk of the step's spp frames, generated + uploaded before the timed region
 
     # multi-GPU exchange: every rank's owned 64x64 tiles go
     # to rank 0 through libmrt's RCCL communicator (include/mrt.h
@@ -478,6 +487,10 @@ def main():
                 r.tiles_write(k, lst[k].numpy()[:mrt.tiles_packed_floats(W, H, k, world)])
 
     def step():
+        if per_frame:   # drawInMTKView: x spp, the image keeps accumulating
+            for _ in range(spp):
+                r.draw_frame()
+            return
         r.reset()
         r.draw(spp)
         if world == 1:
@@ -585,6 +598,13 @@ def main():
              "prepare_tables": int(prep["noise_tables"]),
              "prepare_note": "mrt_renderer_prepare: the window's tables on the library's host threads + one "
                              "upload, per table"}
+    if per_frame:
+        noise.update({"timed_tables": int(st["noise_tables"] - base["noise_tables"]),
+                      "timed_gen_ms": round(st["noise_ms"] - base["noise_ms"], 3),
+                      "timed_noise_waits": int(st["noise_waits"] - base["noise_waits"]),
+                      "timed_prefetched_chunks": int(st["noise_prefetched"] - base["noise_prefetched"]),
+                      "timed_note": "tables generated inside the timed steps on the noise worker thread "
+                                    "(overlapped with rendering); waits = draws that waited for generation"})
 
     result = {
         "metric": METRIC,
@@ -617,6 +637,15 @@ def main():
         "noise_ms_per_frame": noise["noise_ms_per_frame"],
         "noise": noise,
     }
+    if per_frame:
+        result["cadence"] = {
+            "draw_calls": int(st["draws"] - base["draws"]),
+            "draws_overlapped": int(st["draws_overlapped"] - base["draws_overlapped"]),
+            "inflight_waits": int(st["inflight_waits"] - base["inflight_waits"]),
+            "ms_per_draw": round(elapsed * 1e3 / max(1, st["draws"] - base["draws"]), 4),
+            "note": "draws_overlapped: calls enqueued while the previous draw still ran on the GPU; "
+                    "inflight_waits: calls that waited for the draw 3 back (MaxBuffersInFlight, "
+                    "renderer/Renderer.mm:16,593-600)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.shard_of:
         base_cpu, ref_img, mask, frames = cpu_baseline(cfg, args.cpu_frames or spp)
         result["cpu_baseline"] = base_cpu
@@ -626,19 +655,35 @@ def main():
         # same frames through the parity (precise) build
         par = []
         for precise in (args.precise, True) if not args.precise else (True,):
-            if not precise and frames == spp:
+            if not precise and frames == spp and not per_frame:
                 gimg = r.read_image()
                 note = "the timed steps' image (last step: reset + all spp frames)"
             else:
                 r1 = mrt.Renderer(scene, W, H, L, precise=precise)
-                r1.draw(frames)
+                if per_frame:
+                    for _ in range(frames):
+                        r1.draw_frame()
+                else:
+                    r1.draw(frames)
                 gimg = r1.read_image()
                 r1.close()
-                note = f"a separate render of frames 0-{frames - 1}"
+                note = f"a separate render of frames 0-{frames - 1}" + (
+                    " (one mrt_renderer_draw call per frame)" if per_frame else "")
             par.append(image_parity(gimg, ref_img, mask, "precise" if precise else "fast", frames, note))
         result["parity"] = par[0]
         if len(par) > 1:
             result["parity_precise"] = par[1]
+    if per_frame and rank == 0 and world == 1:
+        # the timed progressive image == the same frames drawn in 64-frame
+        # batches (draw_n), bitwise
+        total = int(st["frame_index"])
+        r1 = mrt.Renderer(scene, W, H, L, precise=args.precise)
+        r1.draw(total)
+        same = r1.read_image()[..., :3].tobytes() == r.read_image()[..., :3].tobytes()
+        r1.close()
+        result["image_check"] = (f"timed image (frames 0-{total - 1}, one draw call each) bitwise equal to "
+                                 f"draw_n({total})" if same else "MISMATCH vs draw_n")
+        assert same, "per-frame draws differ from the batched render"
     if world > 1 and args.check_image:
         if rank == 0:   # the exchanged image == one device rendering the whole frame, bitwise
             got = r.read_image()

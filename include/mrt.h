@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 7
+#define MRT_ABI_VERSION 8
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -217,8 +217,19 @@ typedef struct mrt_stats {         /* counters are cumulative since create/resiz
    * table per frame on the CPU before the frame's commit, Renderer.mm:486-496;
    * here mrt_renderer_prepare / draw_n generate a window of tables on the host
    * threads and upload it once) */
-  double noise_ms;                 /* host wall time generating + uploading noise tables */
+  double noise_ms;                 /* host wall time generating noise tables (ABI 8: on the schedule's worker
+                                      thread, overlapped with rendering; uploads are asynchronous) */
   uint64_t noise_tables;           /* per-frame tables generated (noise_ms / noise_tables = cost per frame) */
+  /* ABI 8: the per-frame cadence (drawInMTKView:, Renderer.mm:587-600).  A
+   * draw enqueues its launches without waiting for the GPU: noise tables come
+   * from device chunks of 64 frames generated ahead on a worker thread and
+   * uploaded on their own stream; the one host wait a draw can reach is the
+   * reference's in-flight bound (MaxBuffersInFlight = 3 draws, :16, :593). */
+  uint64_t draws;                  /* draw / draw_n calls that enqueued frames */
+  uint64_t draws_overlapped;       /* draws enqueued while the previous draw was still executing on the GPU */
+  uint64_t inflight_waits;         /* draws that waited for the draw 3 back to finish (the in-flight bound) */
+  uint64_t noise_waits;            /* draws (and prepares) that waited for a chunk's host generation */
+  uint64_t noise_prefetched;       /* chunks the worker generated ahead and a draw found ready */
 } mrt_stats;
 
 int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out);
@@ -229,9 +240,11 @@ int mrt_renderer_resize(mrt_renderer* r, uint32_t width, uint32_t height);
  * by an exchange or mrt_renderer_tiles_write, and an external image, are
  * cleared here); the cumulative counters of mrt_stats are kept. */
 int mrt_renderer_reset(mrt_renderer* r);
-/* Generate + upload the noise tables for frames [frame_index, frame_index+n)
- * ahead of time (the reference regenerates one slot per frame on the CPU,
- * Renderer.mm:486-496).  draw_n calls it itself when needed. */
+/* Generate the noise tables for frames [frame_index, frame_index+n) ahead
+ * of time and enqueue their upload (the reference regenerates one slot per
+ * frame on the CPU, Renderer.mm:486-496).  Blocks on host generation only.
+ * draw_n does the same itself when a chunk is missing, and asks the worker
+ * thread for the next chunk of 64 frames while these render. */
 int mrt_renderer_prepare(mrt_renderer* r, uint32_t n);
 /* One frame: 1 spp, MAX_PATH_LENGTH bounces, running-mean accumulation. */
 int mrt_renderer_draw(mrt_renderer* r);

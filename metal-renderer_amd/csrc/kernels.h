@@ -111,6 +111,13 @@ struct AccumArgs {
   const float4* radiance;      // [batch][num_slots]
   float4* image;
   uint32_t accumulate;         // ACCUMULATE_IMAGE (renderer/Raytracing.h:14); 0: the last frame alone
+  // the last batch of a draw: block 0 copies the draw's statistics words
+  // ([0, copy_words) and [span_word, span_word + span_words)) to the host's
+  // pinned copy and zeroes all zero_words of `counters` for the ring entry's
+  // next draw (no memset and no copy-engine hop per draw); null otherwise
+  uint32_t* counters;
+  uint32_t* host_counters;
+  uint32_t copy_words, span_word, span_words, zero_words;
 };
 
 constexpr uint32_t kShadeDebugMaterial = 1u;   // BounceArgs::flags / launch_shade flags

@@ -2187,6 +2187,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void a
 constexpr uint32_t kAccLoads = 8;
 __global__ __launch_bounds__(kBlock) void accumulate_frame_kernel(AccumArgs a) {
 #endif
+  if (a.counters && blockIdx.x == 0) {   // the draw's render launches have completed (stream order)
+    for (uint32_t i = threadIdx.x; i < a.copy_words; i += kBlock) a.host_counters[i] = a.counters[i];
+    for (uint32_t i = threadIdx.x; i < a.span_words; i += kBlock)
+      a.host_counters[a.span_word + i] = a.counters[a.span_word + i];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.zero_words; i += kBlock) a.counters[i] = 0u;
+    __threadfence_system();
+  }
   for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < a.num_slots; idx += gridDim.x * kBlock) {
     uint32_t x, y;
     slot_pixel(idx, a.shard_rank, a.shard_count, a.tiles_x, x, y);

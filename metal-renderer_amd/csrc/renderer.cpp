@@ -29,6 +29,7 @@
 #include "image.h"
 #include "kernels.h"
 #include "noise.h"
+#include "noise_schedule.h"
 #include "occluders.h"
 #include "primary.h"
 #include "scene.h"
@@ -119,7 +120,8 @@ struct DrawRecord {
   hipEvent_t start = nullptr, stop = nullptr;
   hipEvent_t cleared = nullptr;             // the counters' memset (other render streams of the draw wait on it)
   hipEvent_t copied = nullptr;              // the counters' copy to `host` (read-back stream) is done
-  void* host = nullptr;                     // pinned copy of `counters`, queued behind the draw
+  void* host = nullptr;                     // pinned (device-mapped) copy of `counters`, written behind the draw
+  void* host_dev = nullptr;                 // its device address
   size_t host_bytes = 0;
   std::vector<hipEvent_t> kernel_events;    // MRT_FLAG_PROFILE: 2 per timed bounce launch
   uint32_t frames = 0;
@@ -198,9 +200,12 @@ struct mrt_renderer {
   double wall_khz = 0.0;    // device wall clock (span timestamps; 0 = spans off, MRT_SPANS=0)
   bool image_foreign = false;   // the image holds pixels this renderer did not render (exchange / tiles_write)
   uint32_t grid = 0;        // persistent grid of the bounce kernel
-  // noise: initial table + a window of per-frame tables [noise_first, noise_first + noise_count)
-  DevBuf noise_init, noise_window;
-  int64_t noise_first = 0, noise_count = 0;
+  // noise tables in device chunks of 64 frames, generated ahead on a worker
+  // thread and uploaded on their own stream (noise_schedule.h)
+  std::unique_ptr<mrt::NoiseSchedule> noise;
+  mrt::NoiseSchedule::Counters noise_base;   // the schedule's counters at the last stats reset
+  uint64_t draw_seq = 0;     // draws enqueued (pins the noise chunks a draw reads)
+  uint64_t batch_seq = 0;    // frame batches enqueued (MRT_FLAG_PROFILE times every profile_every-th)
   uint64_t frame_index = 0;
   // Draws in flight: each draw records its survivor counters and events in
   // its own ring entry, and its statistics are read back lazily (when the
@@ -210,6 +215,7 @@ struct mrt_renderer {
   uint32_t draw_next = 0;   // ring entry of the next draw (= the oldest pending one)
   uint32_t profile_every = 8;   // time the launches of every n-th batch (MRT_PROFILE_EVERY)
   uint32_t batch = 1;           // frames per bounce launch (frame batching)
+  bool counter_fold = true;     // draw statistics copied + cleared by the last accumulate (MRT_COUNTER_FOLD)
   mrt_stats stats{};
   uint32_t stack_entries = 32;
   bool stream_allowed = false;  // streaming wavefront possible for this scene / configuration
@@ -289,37 +295,21 @@ int finalize_pending(mrt_renderer* r) {
   return MRT_OK;
 }
 
-int ensure_noise(mrt_renderer* r, int64_t f0, uint32_t n) {
-  if (!r->noise_init.p) {
-    std::vector<float> t(mrt::kNoiseFloats);
-    mrt::make_noise_table(r->desc.seed, -1, t.data());
-    HIP_TRY(upload(r->noise_init, t.data(), t.size() * 4));
+// the noise chunks of frames [f0, f0 + n): generated (host threads, unless
+// the worker already has) and uploaded asynchronously; never waits for the GPU
+int acquire_noise(mrt_renderer* r, int64_t f0, uint32_t n, std::vector<mrt::NoiseSchedule::Chunk*>* out) {
+  using NS = mrt::NoiseSchedule;
+  HIP_TRY(r->noise->poll());
+  const int64_t k0 = NS::chunk_of(f0), k1 = NS::chunk_of(f0 + (int64_t)n - 1);
+  const uint64_t waits = r->noise->counters().waits;
+  for (int64_t k = k0; k <= k1; ++k) {
+    NS::Chunk* c = nullptr;
+    HIP_TRY(r->noise->acquire(k, r->draw_seq, &c));
+    if (out) out->push_back(c);
   }
-  // window [f0 - 2, f0 + n): frames < 0 hold the initial table, so a kernel
-  // addresses T_{f - c} for every iteration without a select
-  const int64_t lo = f0 - 2, hi = f0 + (int64_t)n;
-  if (r->noise_window.p && lo >= r->noise_first && hi <= r->noise_first + r->noise_count) return MRT_OK;
-  const int64_t count = hi - lo;
-  const auto t0 = std::chrono::steady_clock::now();
-  std::vector<float> host((size_t)count * mrt::kNoiseFloats);
-  const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      for (int64_t k = t; k < count; k += nt)   // MRT_FLAG_STATIC_NOISE (ANIMATE_NOISE 0): the initial table for every frame
-        mrt::make_noise_table(r->desc.seed, lo + k < 0 || (r->desc.flags & MRT_FLAG_STATIC_NOISE) ? -1 : lo + k,
-                              host.data() + (size_t)k * mrt::kNoiseFloats);
-    });
-  for (auto& x : th) x.join();
-  const auto t1 = std::chrono::steady_clock::now();
-  { int rc = finalize_pending(r); if (rc) return rc; }
-  HIP_TRY(hipStreamSynchronize(r->stream));   // (the wait for queued draws is not noise cost)
-  const auto t2 = std::chrono::steady_clock::now();
-  HIP_TRY(upload(r->noise_window, host.data(), host.size() * 4));
-  r->noise_first = lo;
-  r->noise_count = count;
-  r->stats.noise_ms += std::chrono::duration<double, std::milli>((t1 - t0) + (std::chrono::steady_clock::now() - t2)).count();
-  r->stats.noise_tables += (uint64_t)count;
+  if (r->noise->counters().waits != waits) r->stats.noise_waits += 1;
+  // the next chunk's tables are generated while these frames render
+  r->noise->prefetch(k1 + 1);
   return MRT_OK;
 }
 
@@ -377,6 +367,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
   r->image_foreign = false;
   r->frame_index = 0;
   r->stats = mrt_stats{};
+  r->noise_base = r->noise->counters();
   r->stats.owned_pixels = r->owned_pixels;
   r->stats.kernel = r->path_mode ? 1u : (r->stream_mode ? 2u : 0u);
   r->stats.inflight = r->inflight;
@@ -1261,6 +1252,7 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   }
   r->own_image = desc->image == nullptr;
   r->image = desc->image;
+  r->noise = std::make_unique<mrt::NoiseSchedule>(desc->seed, (desc->flags & MRT_FLAG_STATIC_NOISE) != 0);
   for (DrawRecord& d : r->draws) {
     HIP_TRY(hipEventCreate(&d.start));
     HIP_TRY(hipEventCreate(&d.stop));
@@ -1285,6 +1277,7 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   if (need > r->stack_entries)   // spill variants: 8 / 12 (path kernel; the wavefront runs 16) / 16 / 32
     r->stack_entries = r->stack_entries <= 8 ? 8 : r->stack_entries <= 12 ? 12 : r->stack_entries <= 16 ? 16 : 32;
   if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
+  if (const char* v = std::getenv("MRT_COUNTER_FOLD")) r->counter_fold = std::atoi(v) != 0;
   if (const char* v = std::getenv("MRT_PROFILE_EVERY"))
     r->profile_every = std::max<uint32_t>(1, (uint32_t)std::strtoul(v, nullptr, 0));
   {
@@ -1386,7 +1379,7 @@ int mrt_renderer_reset(mrt_renderer* r) {
 
 int mrt_renderer_prepare(mrt_renderer* r, uint32_t n) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");
-  return ensure_noise(r, (int64_t)r->frame_index, std::max<uint32_t>(1, n));
+  return acquire_noise(r, (int64_t)r->frame_index, std::max<uint32_t>(1, n), nullptr);
 }
 
 int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
@@ -1395,20 +1388,49 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     n = r->frame_index >= r->max_frames ? 0u : (uint32_t)std::min<uint64_t>(n, r->max_frames - r->frame_index);
   if (n == 0) return MRT_OK;
   DrawRecord& d = r->draws[r->draw_next];
-  int rc = finalize_draw(r, d);   // the ring entry's previous draw (kDrawRing draws back)
+  // at most kDrawRing (3) draws in flight: the ring entry's previous draw must
+  // have finished — the reference's MaxBuffersInFlight semaphore
+  // (renderer/Renderer.mm:16, :593-600), the only host wait of a draw
+  if (d.pending && hipEventQuery(d.copied) == hipErrorNotReady) r->stats.inflight_waits += 1;
+  int rc = finalize_draw(r, d);
   if (rc) return rc;
-  rc = ensure_noise(r, (int64_t)r->frame_index, n);
+  r->draw_seq += 1;
+  std::vector<mrt::NoiseSchedule::Chunk*> chunks;
+  rc = acquire_noise(r, (int64_t)r->frame_index, n, &chunks);
   if (rc) return rc;
   const uint32_t L = r->desc.max_path_length;
   const uint32_t B = r->batch;
-  const uint32_t nb = (n + B - 1) / B;   // launches of up to B frames each
+  // frame batches of up to B frames, none crossing a noise chunk (64 frames,
+  // a multiple of B): a 64-frame draw from a multiple of 64 is one batch
+  struct Batch { uint64_t f; uint32_t frames; mrt::NoiseSchedule::Chunk* noise; };
+  std::vector<Batch> batches;
+  for (uint64_t f = r->frame_index, end = r->frame_index + n; f < end;) {
+    const int64_t k = mrt::NoiseSchedule::chunk_of((int64_t)f);
+    const uint64_t chunk_end = (uint64_t)(k + 1) * mrt::NoiseSchedule::kChunkFrames;
+    const uint32_t b = (uint32_t)std::min<uint64_t>({(uint64_t)B, end - f, chunk_end - f});
+    batches.push_back({f, b, chunks[(size_t)(k - mrt::NoiseSchedule::chunk_of((int64_t)r->frame_index))]});
+    f += b;
+  }
+  const uint32_t nb = (uint32_t)batches.size();
   // survivor counters [nb * L] and, 128-B aligned after them, the grab
   // counters of every launch of the draw: zeroed by ONE memset
   const size_t grab_words = (size_t)mrt::kGrabRanges * mrt::kGrabStride;
   const size_t grab_off = ((size_t)nb * L + 31) / 32 * 32;   // words
   const size_t span_off = (grab_off + (size_t)nb * L * grab_words + 1) / 2 * 8;   // bytes, 8-B aligned
   const size_t counter_bytes = span_off + (size_t)nb * 16;
-  if (d.counters.bytes < counter_bytes) HIP_TRY(d.counters.alloc(counter_bytes));
+  bool fresh = false;
+  if (d.counters.bytes < counter_bytes) {
+    HIP_TRY(d.counters.alloc(counter_bytes));
+    fresh = true;
+  }
+  if (d.host_bytes < counter_bytes) {
+    if (d.host) HIP_TRY(hipHostFree(d.host));
+    d.host = d.host_dev = nullptr;
+    d.host_bytes = 0;
+    HIP_TRY(hipHostMalloc(&d.host, counter_bytes, hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer(&d.host_dev, d.host, 0));
+    d.host_bytes = counter_bytes;
+  }
   const uint32_t launches_per_batch = r->path_mode || r->stream_mode ? 1u : L;
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
@@ -1421,12 +1443,16 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   }
   HIP_TRY(hipEventRecord(d.start, r->stream));
   // The render launches never wait on the main stream (it only carries
-  // accumulates and image work; the noise window is uploaded synchronously):
-  // the counters are cleared on the first batch's render stream and the
-  // draw's other render streams wait for that.
+  // accumulates and image work; a noise chunk's upload is waited for through
+  // its own event): the counters are cleared on the first batch's render
+  // stream and the draw's other render streams wait for that.
+  // The draw's last accumulate copies its statistics to the pinned host copy
+  // and zeroes the counters for the ring entry's next draw (whose host side
+  // has waited for that accumulate in finalize_draw): a fresh buffer is the
+  // only one to clear here.  MRT_COUNTER_FOLD=0: memset + copy per draw.
   const uint32_t s0 = r->slot_next;
-  HIP_TRY(hipMemsetAsync(d.counters.p, 0, counter_bytes, r->slots[s0].stream));
-  if (r->inflight > 1 && nb > 1) {
+  if (fresh || !r->counter_fold) HIP_TRY(hipMemsetAsync(d.counters.p, 0, d.counters.bytes, r->slots[s0].stream));
+  if ((fresh || !r->counter_fold) && r->inflight > 1 && nb > 1) {
     HIP_TRY(hipEventRecord(d.cleared, r->slots[s0].stream));
     for (uint32_t j = 1; j < std::min(nb, r->inflight); ++j)
       HIP_TRY(hipStreamWaitEvent(r->slots[(s0 + j) % r->inflight].stream, d.cleared, 0));
@@ -1434,12 +1460,23 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   uint32_t* cnt = d.counters.as<uint32_t>();
   size_t ev = 0;
   for (uint32_t k = 0; k < nb; ++k) {
-    const uint64_t f = r->frame_index + (uint64_t)k * B;
-    const uint32_t batch = std::min<uint32_t>(B, n - k * B);
-    FrameSlot& fs = r->slots[(s0 + k) % r->inflight];
+    const uint64_t f = batches[k].f;
+    const uint32_t batch = batches[k].frames;
+    mrt::NoiseSchedule::Chunk* nc = batches[k].noise;
+    const uint32_t slot = (s0 + k) % r->inflight;
+    FrameSlot& fs = r->slots[slot];
     const bool own = fs.stream != r->stream;
-    // the slot's radiance is free once the accumulate that last read it ran
+    // the slot's radiance is free once the accumulate that last read it ran.
+    // (Rotating batch-sized regions of it instead, so that a single-frame
+    // draw waits only once per 64 frames, measured -1.1 % on the per-frame
+    // cadence: the next kernel then competes with the accumulates for CUs.)
     if (own && fs.acc_recorded) HIP_TRY(hipStreamWaitEvent(fs.stream, fs.acc_done, 0));
+    float4* radiance = fs.radiance.as<float4>();
+    // the noise chunk's upload (once per chunk upload and render stream)
+    if (!(nc->waited_streams & (1u << slot))) {
+      HIP_TRY(hipStreamWaitEvent(fs.stream, nc->ready, 0));
+      nc->waited_streams |= 1u << slot;
+    }
     uint32_t* seg = fs.segments.as<uint32_t>();
     uint32_t* meta = seg + 4 * (size_t)r->grid;
     for (uint32_t b = 0; b < launches_per_batch; ++b) {
@@ -1467,9 +1504,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
         a.in_q.plane[p] = fs.queue[b & 1][p].as<float4>();
         a.out_q.plane[p] = fs.queue[(b + 1) & 1][p].as<float4>();
       }
-      a.noise_window = r->noise_window.as<float4>();
-      a.noise_offset = (uint32_t)((int64_t)f - r->noise_first);
-      a.radiance = fs.radiance.as<float4>();
+      a.noise_window = static_cast<const float4*>(nc->dev);
+      a.noise_offset = (uint32_t)((int64_t)f - mrt::NoiseSchedule::first_frame(mrt::NoiseSchedule::chunk_of((int64_t)f)));
+      a.radiance = radiance;
       a.stack_spill = fs.spill.as<uint32_t>();
       a.bounce_counts = cnt + (size_t)k * L;
       a.primary = r->primary.as<uint32_t>();
@@ -1477,7 +1514,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.span = r->wall_khz > 0.0
                    ? reinterpret_cast<unsigned long long*>(static_cast<char*>(d.counters.p) + span_off) + 2 * k
                    : nullptr;
-      const bool timed = profile && (k % r->profile_every) == 0;
+      const bool timed = profile && (r->batch_seq % r->profile_every) == 0;
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
       if (r->path_mode) HIP_TRY(launch_paths(r, a, fs.stream));
       else if (r->stream_mode) HIP_TRY(launch_stream(r, a, fs.stream));
@@ -1499,25 +1536,39 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     acc.shard_count = r->desc.shard_count;
     acc.tiles_x = r->tiles_x;
     acc.num_slots = r->owned_tiles * 4096u;
-    acc.radiance = fs.radiance.as<float4>();
+    acc.radiance = radiance;
     acc.image = reinterpret_cast<float4*>(r->image);
     acc.accumulate = (r->desc.flags & MRT_FLAG_NO_ACCUMULATE) ? 0u : 1u;
+    if (k + 1 == nb && r->counter_fold) {
+      acc.counters = d.counters.as<uint32_t>();
+      acc.host_counters = static_cast<uint32_t*>(d.host_dev);
+      acc.copy_words = nb * L;
+      acc.span_word = (uint32_t)(span_off / 4);
+      acc.span_words = nb * 4;
+      acc.zero_words = (uint32_t)(d.counters.bytes / 4);
+    }
     HIP_TRY(launch_accumulate_frame(r, acc, r->stream));
     HIP_TRY(hipEventRecord(fs.acc_done, r->stream));
     fs.acc_recorded = true;
+    r->batch_seq += 1;
   }
   r->slot_next = (s0 + nb) % r->inflight;
   HIP_TRY(hipEventRecord(d.stop, r->stream));
-  if (d.host_bytes < counter_bytes) {
-    if (d.host) HIP_TRY(hipHostFree(d.host));
-    d.host = nullptr;
-    d.host_bytes = 0;
-    HIP_TRY(hipHostMalloc(&d.host, counter_bytes, hipHostMallocDefault));
-    d.host_bytes = counter_bytes;
+  // the chunks' buffers are reusable once this draw's accumulates (which
+  // follow every render launch of the draw) have run
+  for (mrt::NoiseSchedule::Chunk* c : chunks) {
+    HIP_TRY(hipEventRecord(c->last_use, r->stream));
+    c->used = true;
   }
+  {   // enqueued while the previous draw is still rendering (frames in flight)
+    const DrawRecord& prev = r->draws[(r->draw_next + kDrawRing - 1) % kDrawRing];
+    if (prev.pending && hipEventQuery(prev.stop) == hipErrorNotReady) r->stats.draws_overlapped += 1;
+  }
+  r->stats.draws += 1;
   // (no stream of its own: a process has few hardware queues — 4 by
   // default — and two streams sharing one serialise their launches)
-  HIP_TRY(hipMemcpyAsync(d.host, d.counters.p, counter_bytes, hipMemcpyDeviceToHost, r->stream));
+  if (!r->counter_fold)
+    HIP_TRY(hipMemcpyAsync(d.host, d.counters.p, counter_bytes, hipMemcpyDeviceToHost, r->stream));
   HIP_TRY(hipEventRecord(d.copied, r->stream));
   d.pending = true;
   d.frames = n;
@@ -1674,6 +1725,10 @@ int mrt_renderer_stats(const mrt_renderer* r, mrt_stats* stats) {
   int rc = finalize_pending(const_cast<mrt_renderer*>(r));
   if (rc) return rc;
   *stats = r->stats;
+  const mrt::NoiseSchedule::Counters& c = r->noise->counters();
+  stats->noise_ms = c.gen_ms - r->noise_base.gen_ms;
+  stats->noise_tables = c.tables - r->noise_base.tables;
+  stats->noise_prefetched = c.prefetched - r->noise_base.prefetched;
   return MRT_OK;
 }
 
@@ -1705,6 +1760,7 @@ int mrt_renderer_destroy(mrt_renderer* r) {
     if (d.copied) (void)hipEventDestroy(d.copied);
     if (d.host) (void)hipHostFree(d.host);
   }
+  r->noise.reset();   // joins the worker; the draws reading its chunks have finished (stream synchronised above)
   if (r->own_stream) (void)hipStreamDestroy(r->stream);
   delete r;
   return MRT_OK;

@@ -122,6 +122,8 @@ class Stats(ctypes.Structure):
         ("span_ms", ctypes.c_double), ("spans", ctypes.c_uint64),
         ("primary_blocks", ctypes.c_uint32), ("primary_mean", ctypes.c_float),
         ("noise_ms", ctypes.c_double), ("noise_tables", ctypes.c_uint64),
+        ("draws", ctypes.c_uint64), ("draws_overlapped", ctypes.c_uint64), ("inflight_waits", ctypes.c_uint64),
+        ("noise_waits", ctypes.c_uint64), ("noise_prefetched", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -376,6 +378,12 @@ class Renderer:
     # -drawInMTKView:
     def draw(self, frames: int = 1) -> None:
         _check(lib().mrt_renderer_draw_n(self._h, frames), "mrt_renderer_draw_n")
+
+    def draw_frame(self) -> None:
+        """One drawInMTKView: frame (mrt_renderer_draw, 1 spp): enqueued
+        without waiting for the GPU (at most 3 draws in flight, the
+        reference's MaxBuffersInFlight)."""
+        _check(lib().mrt_renderer_draw(self._h), "mrt_renderer_draw")
 
     def set_max_frames(self, n: int) -> None:
         """MAX_FRAMES (Renderer.mm:589-590): draws past frame n are no-ops (0 = unlimited)."""

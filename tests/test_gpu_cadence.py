@@ -1,0 +1,118 @@
+"""GPU: the reference's per-frame cadence — one drawInMTKView: per call,
+1 spp, at most MaxBuffersInFlight = 3 command buffers in flight
+(renderer/Renderer.mm:16, :587-638), the noise table regenerated on the CPU for
+every frame (:472-498).
+
+mrt_renderer_draw must enqueue without waiting for the GPU (noise tables come
+from device chunks of 64 frames generated ahead on a worker thread and
+uploaded on their own stream, csrc/noise_schedule.h), and a frame drawn on its
+own must render exactly what the same frame renders inside a 64-frame batch
+(draw_n), in both builds — so the per-frame path inherits draw_n's bitwise
+parity with the oracle (test_gpu_configs.py, test_gpu_parity.py)."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def box(mrt_mod):
+    return mrt_mod.Scene("cornellbox")
+
+
+def _img(r):
+    return r.read_image()[..., :3].tobytes()
+
+
+@pytest.mark.parametrize("precise", [True, False])
+def test_per_frame_draws_equal_batched_draw(gpu, mrt_mod, box, precise):
+    """70 single-frame draws (crossing the 64-frame noise chunk) == draw_n(70)."""
+    W, H, L, n = 320, 200, 4, 70
+    a = mrt_mod.Renderer(box, W, H, L, precise=precise)
+    for _ in range(n):
+        a.draw_frame()
+    sa = a.stats()
+    b = mrt_mod.Renderer(box, W, H, L, precise=precise)
+    b.draw(n)
+    sb = b.stats()
+    assert _img(a) == _img(b)
+    assert sa["active_ray_bounces"] == sb["active_ray_bounces"] and sa["frame_index"] == n
+    assert sa["draws"] == n and sb["draws"] == 1
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("cut", [30, 63, 64, 65])
+def test_draw_across_noise_chunks(gpu, mrt_mod, box, cut):
+    """A draw whose frames straddle a chunk boundary is split there into
+    batches that each address one chunk: draw_n(cut) + draw_n(150 - cut) ==
+    draw_n(150), bitwise (precise build)."""
+    W, H, L = 256, 160, 3
+    a = mrt_mod.Renderer(box, W, H, L, precise=True)
+    a.draw(cut)
+    a.draw(150 - cut)
+    b = mrt_mod.Renderer(box, W, H, L, precise=True)
+    b.draw(150)
+    assert _img(a) == _img(b)
+    a.close()
+    b.close()
+
+
+def test_frame_draws_are_enqueued_ahead_of_the_gpu(gpu, mrt_mod, box):
+    """At 1080p a 1-spp frame takes ~0.2 ms of GPU time and a draw call far
+    less host time, so with no host wait in the draw path each call returns
+    while the previous draw is still executing: most draws are counted as
+    overlapped (the previous draw's stop event not yet complete when the
+    call returns), and the only waits are the in-flight bound's."""
+    W, H, L = 1920, 1080, 4
+    r = mrt_mod.Renderer(box, W, H, L)
+    r.draw_frame()
+    r.sync()
+    s0 = r.stats()
+    n = 128
+    for _ in range(n):
+        r.draw_frame()
+    r.sync()
+    s1 = r.stats()
+    draws = s1["draws"] - s0["draws"]
+    overlapped = s1["draws_overlapped"] - s0["draws_overlapped"]
+    waits = s1["inflight_waits"] - s0["inflight_waits"]
+    assert draws == n
+    assert overlapped >= n // 2, (overlapped, waits)
+    # the worker generated the next chunk of tables while the frames of the
+    # current one rendered: no draw waited for noise past the first chunk
+    assert s1["noise_waits"] - s0["noise_waits"] == 0, s1
+    assert s1["noise_prefetched"] >= 2, s1
+    r.close()
+
+
+def test_reset_reuses_resident_noise(gpu, mrt_mod, box):
+    """A reset back to frame 0 finds chunk 0 on the device: no table is
+    generated again (the bench's batched steps), and the image is the same."""
+    W, H, L = 200, 120, 4
+    r = mrt_mod.Renderer(box, W, H, L, precise=True)
+    r.draw(64)
+    first = _img(r)
+    s0 = r.stats()
+    r.reset()
+    r.draw(64)
+    assert _img(r) == first
+    # chunk 0 is not generated again: no draw waited for noise, and the only
+    # tables uploaded since are the worker's prefetch of chunk 1 (66 tables)
+    s1 = r.stats()
+    assert s1["noise_waits"] == s0["noise_waits"]
+    assert s1["noise_tables"] - s0["noise_tables"] in (0, 66)
+    r.close()
+
+
+def test_static_noise_per_frame(gpu, mrt_mod, box):
+    """ANIMATE_NOISE 0 through the per-frame path: every chunk holds the
+    initial table; bitwise equal to draw_n."""
+    W, H, L = 128, 96, 4
+    a = mrt_mod.Renderer(box, W, H, L, precise=True, animate_noise=False)
+    for _ in range(5):
+        a.draw_frame()
+    b = mrt_mod.Renderer(box, W, H, L, precise=True, animate_noise=False)
+    b.draw(5)
+    assert _img(a) == _img(b)
+    a.close()
+    b.close()

@@ -9,7 +9,8 @@ export TMPDIR=/tmp
 # overlap consecutive launches, which stretches each launch's trace span
 # (the bench times them by device spans instead); counters per launch are
 # the same either way
-export MRT_INFLIGHT=${MRT_INFLIGHT:-1}
+INF=${MRT_INFLIGHT:-1}
+export MRT_INFLIGHT=$INF
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
 # the library these passes measure (bench.py compares it with the one it loads)
@@ -28,7 +29,7 @@ step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -f csv -- $
 # is the kernel's share of the step the bench times
 export MRT_INFLIGHT=2
 step trace2 300 rocprofv3 --kernel-trace -d $OUT/trace2 -o run -f csv -- $BENCH
-export MRT_INFLIGHT=1
+export MRT_INFLIGHT=$INF
 step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/fetch -o run -f csv -- $BENCH
 step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/write -o run -f csv -- $BENCH
 step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/sq -o run -f csv -- $BENCH
