@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <array>
 #include <deque>
@@ -318,7 +319,10 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
   const std::vector<BuildNode>& bn = b.nodes;
   const uint32_t W = opt.width;
   auto is_leaf = [&](int32_t id) { return bn[id].child[0] < 0; };
-  const bool dp = opt.collapse_dp && W == 4;
+  bool dp = opt.collapse_dp > 0 || (opt.collapse_dp < 0 && num_triangles < kGreedyCollapseTriangles);
+  if (opt.collapse_dp < 0)
+    if (const char* v = std::getenv("MRT_COLLAPSE")) dp = std::atoi(v) != 0;   // 0: greedy, 1: DP
+  dp = dp && W == 4;
   std::vector<std::array<float, 4>> best;
   std::vector<std::array<uint8_t, 4>> pick;   // k1 of the split (0: m is one slot)
   std::vector<uint8_t> inner;                 // m as a wide node: k1 of its children's slots (k2 = 4 - k1 at most)

@@ -863,7 +863,11 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
 // (tri_bary over the shading record's vertices: the leaf record's v0,
 // e1 = v1 - v0, e2 = v2 - v0 are the same float operations, bvh.cpp) and its
 // acceptance rule, so "occluded" here is the traversal's answer and
-// "not occluded" changes nothing.  Scenes of >= kOriginTestTriangles only
+// "not occluded" changes nothing — bit-exactly in the precise build (no FMA
+// contraction).  In the fast build (-ffp-contract=fast) the compiler may fuse
+// this inlined copy of tri_bary differently from the leaf loop's, so on a
+// near-tie (t within an ulp of t_T or 0) the two can disagree; the fast
+// build's 1e-2 image gate covers such flips.  Scenes of >= kOriginTestTriangles only
 // (DeviceScene::origin_test; MRT_ORIGIN_TEST=0 compiles it out).
 #ifndef MRT_ORIGIN_TEST
 #define MRT_ORIGIN_TEST 1

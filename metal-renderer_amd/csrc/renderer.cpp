@@ -699,12 +699,10 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (const char* v = std::getenv("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
   if (const char* v = std::getenv("MRT_BINS")) opt.bins = (uint32_t)std::strtoul(v, nullptr, 0);
   if (const char* v = std::getenv("MRT_EXACT_SAH")) opt.exact_sah_below = (uint32_t)std::strtoul(v, nullptr, 0);
-  // the area-optimal BVH4 collapse (bvh.cpp) for scenes below 64 K
-  // triangles: C2 +0.8 %, C3 +1.9 %, C3g +0.5 %; the 1M-triangle C4 tree
-  // (21 % fewer, fuller nodes: more children pushed per step) -1.2 %, so it
-  // keeps the greedy collapse (r4, alternating in one call)
-  opt.collapse_dp = T < mrt::kGreedyCollapseTriangles;
-  if (const char* v = std::getenv("MRT_COLLAPSE")) opt.collapse_dp = std::atoi(v) != 0;   // 0: greedy, 1: DP
+  // BVH4 collapse: opt.collapse_dp's size policy (bvh.h), the same for every
+  // build path — the area-optimal collapse below 64 K triangles: C2 +0.8 %,
+  // C3 +1.9 %, C3g +0.5 %; the 1M-triangle C4 tree (21 % fewer, fuller
+  // nodes: more children pushed per step) -1.2 %, so greedy there (r4)
   const uint32_t builder = desc->bvh_builder ? desc->bvh_builder : MRT_BVH_HOST_SAH;
   // BVH4 is the one layout the kernels traverse (BVH2 measured -24 %, a
   // compressed BVH8 -33 % and a quantised BVH4 -10 % on C4 in r2)

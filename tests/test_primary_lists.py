@@ -19,7 +19,7 @@ def checker(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("primary") / "primary_check")
     srcs = [os.path.join(ROOT, "tools", "primary_check.cpp")] + [os.path.join(CSRC, f + ".cpp")
                                                                    for f in ("scene", "bvh", "primary")]
-    subprocess.run(["g++", "-O2", "-mfma", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", exe] + srcs, check=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-o", exe] + srcs, check=True)
     return exe
 
 
