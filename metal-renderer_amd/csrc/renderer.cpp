@@ -856,6 +856,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     in.occluder_margin = occ.margin;
     in.occluder_max_stack = ob.max_stack;
     in.occluder_cos_min = occ.cos_min;
+    in.occluder_exit_margin = occ.exit_margin;
+    for (size_t k = 0; k < occ.planes.size() && k < 8; ++k)
+      for (int c = 0; c < 4; ++c) in.occluder_plane[k][c] = occ.planes[k][c];
   }
   in.vertices = (uint32_t)h.vertices.size();
   in.triangles = T;
@@ -915,6 +918,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     d.occ_planes = (uint32_t)occ.planes.size();
     d.occ_margin = occ.margin;
     d.occ_cos_min = occ.cos_min;
+    d.occ_exit_margin = occ.exit_margin;
     for (uint32_t k = 0; k < d.occ_planes; ++k)
       for (int c = 0; c < 4; ++c) d.occ_plane[k][c] = occ.planes[k][c];
     d.max_stack = std::max(d.max_stack, ob.max_stack);

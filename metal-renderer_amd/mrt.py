@@ -97,7 +97,13 @@ class SceneInfo(ctypes.Structure):
         ("occluder_planes", ctypes.c_uint32), ("occluder_culled", ctypes.c_uint32),
         ("occluder_nodes", ctypes.c_uint32), ("occluder_margin", ctypes.c_float),
         ("occluder_max_stack", ctypes.c_uint32), ("occluder_cos_min", ctypes.c_float),
+        ("occluder_exit_margin", ctypes.c_float), ("occluder_plane", (ctypes.c_float * 4) * 8),
     ]
+
+
+def _plain(v):
+    """ctypes arrays (nested) to lists; scalars unchanged."""
+    return [_plain(x) for x in v] if isinstance(v, ctypes.Array) else v
 
 
 class RendererDesc(ctypes.Structure):
@@ -259,7 +265,7 @@ class Scene:
         self._h = h
         info = SceneInfo()
         _check(lib().mrt_scene_info_get(h, ctypes.byref(info)), "mrt_scene_info_get")
-        self.info = {k: getattr(info, k) for k, _ in SceneInfo._fields_}
+        self.info = {k: _plain(getattr(info, k)) for k, _ in SceneInfo._fields_}
 
     @property
     def handle(self):
