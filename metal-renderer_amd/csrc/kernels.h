@@ -60,6 +60,23 @@ constexpr uint32_t kStreamCap = 128;
 constexpr uint32_t kStreamMaxL = 64;
 inline size_t stream_slots(uint32_t L, uint32_t G) { return (size_t)G * 4 * (L > 1 ? L - 1 : 1) * kStreamCap; }
 
+// n / d for every n < 2^31 as mulhi(n, m) >> sh (m = 0: d = 1), with
+// l = ceil(log2 d), m = ceil(2^(31 + l) / d) < 2^32, sh = l - 1: the error
+// m d - 2^(31+l) < d <= 2^l, so n (m d - 2^(31+l)) < 2^(31+l) and the
+// floor is exact (Granlund & Montgomery 1994, N = 31).  Wave-uniform kernel
+// arguments: the quotient costs one v_mul_hi_u32 and a shift instead of the
+// compiler's per-lane reciprocal sequence and its three VGPRs.
+struct MagicDiv {
+  uint32_t m, sh;
+};
+inline MagicDiv magic_div(uint32_t d) {
+  if (d <= 1) return {0u, 0u};
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const unsigned long long p = 1ull << (31 + l);
+  return {(uint32_t)((p + d - 1) / d), l - 1};
+}
+
 struct BounceArgs {
   uint32_t width, height;
   uint32_t frame_index;        // SharedData.frameIndex of the batch's first frame
@@ -99,6 +116,9 @@ struct BounceArgs {
                                // (wall_clock64 ticks; null = not recorded)
   const uint32_t* primary;     // camera-ray candidate lists per 8x8 pixel block (primary.h; null = traverse)
   uint32_t primary_bx;         // blocks per row of `primary`
+  // exact division by the launch's runtime divisors without per-lane
+  // reciprocals (magic_div): tiles_x, num_slots, batch
+  MagicDiv div_tiles, div_slots, div_batch;
 };
 
 // running-mean accumulation of one frame over the owned tiles

@@ -1162,6 +1162,30 @@ __device__ __forceinline__ void slot_pixel(uint32_t s, uint32_t rank, uint32_t c
   y = ty * kTile + (blk >> 3) * 8u + (q >> 3);
 }
 
+#ifndef MRT_MAGIC_DIV
+#define MRT_MAGIC_DIV 1
+#endif
+// n / d for n < 2^31 through the launch's magic (kernels.h MagicDiv), or the
+// plain division (MRT_MAGIC_DIV=0)
+__device__ __forceinline__ uint32_t mdiv(uint32_t n, MagicDiv m, uint32_t d) {
+#if MRT_MAGIC_DIV
+  (void)d;
+  return m.m ? (__umulhi(n, m.m) >> m.sh) : n;
+#else
+  (void)m;
+  return n / d;
+#endif
+}
+// slot_pixel with the launch's magic for tiles_x
+__device__ __forceinline__ void slot_pixel_a(uint32_t s, const BounceArgs& a, uint32_t& x, uint32_t& y) {
+  const uint32_t k = s >> 12, p = s & 4095u;
+  const uint32_t t = a.shard_rank + k * a.shard_count;
+  const uint32_t ty = mdiv(t, a.div_tiles, a.tiles_x), tx = t - ty * a.tiles_x;
+  const uint32_t blk = p >> 6, q = p & 63u;
+  x = tx * kTile + (blk & 7u) * 8u + (q & 7u);
+  y = ty * kTile + (blk >> 3) * 8u + (q >> 3);
+}
+
 // noise table of frame (batch frame fj) - back, back in {0, 1, 2}
 __device__ __forceinline__ const float4* noise_table(const BounceArgs& a, uint32_t fj, uint32_t back) {
   return a.noise_window + (a.noise_offset + fj - back) * (kNoiseDim * kNoiseDim);
@@ -1438,9 +1462,9 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
     if (bounce == 0) {
       // frame fj of the batch (num_slots is a multiple of 4096: waves never
       // straddle frames, so fj is wave-uniform)
-      const uint32_t fj = a.batch == 1u ? 0u : __builtin_amdgcn_readfirstlane(idx / a.num_slots);
+      const uint32_t fj = a.batch == 1u ? 0u : __builtin_amdgcn_readfirstlane(mdiv(idx, a.div_slots, a.num_slots));
       uint32_t x, y;
-      slot_pixel(idx - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+      slot_pixel_a(idx - fj * a.num_slots, a, x, y);
       active = (x < a.width) && (y < a.height);
       if (active) {
         tag = idx;
@@ -1518,9 +1542,9 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
     LS_ADD(13, (uint32_t)__popcll(__ballot(hit_ok)));
   }
   if (hit_ok) {
-    const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;   // frame in batch
+    const uint32_t fj = a.batch == 1u ? 0u : mdiv(gslot, a.div_slots, a.num_slots);   // frame in batch
     uint32_t x, y;
-    slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+    slot_pixel_a(gslot - fj * a.num_slots, a, x, y);
     const uint32_t back = (bounce % 3u) == 0 ? 0u : ((bounce % 3u) == 1 ? 2u : 1u);   // uniform
     const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, bounce, a.frame_index + fj)];
     if (a.debug & 2u) {   // ablation: no shading, reflect back along the ray
@@ -2037,15 +2061,15 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         // geometry in that XCD's L2
         uint32_t fj, sl;
         if (sc.region_grabs) {
-          const uint32_t q = idx >> 6, blk = q / a.batch;
+          const uint32_t q = idx >> 6, blk = mdiv(q, a.div_batch, a.batch);
           fj = q - blk * a.batch;
           sl = (blk << 6) | (idx & 63u);
         } else {
-          fj = a.batch == 1u ? 0u : idx / a.num_slots;
+          fj = a.batch == 1u ? 0u : mdiv(idx, a.div_slots, a.num_slots);
           sl = idx - fj * a.num_slots;
         }
         uint32_t x, y;
-        slot_pixel(sl, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+        slot_pixel_a(sl, a, x, y);
         if ((x < a.width) && (y < a.height)) {
           const float4 ns = noise_table(a, fj, 0u)[(x % kNoiseDim) + (y % kNoiseDim) * kNoiseDim];
           camera_ray(x, y, a.width, a.height, ns, ro, rd);
@@ -2133,9 +2157,9 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       sh.valid = false;
       LS_ADD(13, (uint32_t)__popcll(__ballot(hit_ok)));
       if (hit_ok) {
-        const uint32_t fj = a.batch == 1u ? 0u : gslot / a.num_slots;
+        const uint32_t fj = a.batch == 1u ? 0u : mdiv(gslot, a.div_slots, a.num_slots);
         uint32_t x, y;
-        slot_pixel(gslot - fj * a.num_slots, a.shard_rank, a.shard_count, a.tiles_x, x, y);
+        slot_pixel_a(gslot - fj * a.num_slots, a, x, y);
         const uint32_t back = (bounce % 3u) == 0 ? 0u : ((bounce % 3u) == 1 ? 2u : 1u);
         const float4 ns = noise_table(a, fj, back)[shade_noise_cell(x, y, bounce, a.frame_index + fj)];
         shade_hit<MODE>(sc, cx, h, s, ns, bounce, L, !last, sh, (a.flags & kShadeDebugMaterial) != 0);

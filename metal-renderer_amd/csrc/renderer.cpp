@@ -1493,6 +1493,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.shard_count = r->desc.shard_count;
       a.tiles_x = r->tiles_x;
       a.num_slots = r->owned_tiles * 4096u;
+      a.div_tiles = mrt::magic_div(a.tiles_x);
+      a.div_slots = mrt::magic_div(a.num_slots);
+      a.div_batch = mrt::magic_div(batch);
       a.debug = r->debug;
       a.flags = (r->desc.flags & MRT_FLAG_DEBUG_MATERIAL) ? mrt::kShadeDebugMaterial : 0u;
       a.in_segments = 2 * r->grid;   // two material classes per block

@@ -11,7 +11,10 @@ export TMPDIR=/tmp
 # the same either way
 INF=${MRT_INFLIGHT:-1}
 export MRT_INFLIGHT=$INF
-OUT=gpurun_out/prof_${TAG}_${CFG}
+# NAME: the output's config name (default the bench config; e.g. c5s8 for
+# --config c5 --shard-of 8 -> profiles/pmc_c5s8.json via prof_summary.py)
+NAME=${NAME:-$CFG}
+OUT=gpurun_out/prof_${TAG}_${NAME}
 mkdir -p $OUT
 # the library these passes measure (bench.py compares it with the one it loads)
 md5sum metal-renderer_amd/lib/libmrt.so | cut -d' ' -f1 > $OUT/lib.md5

@@ -10,8 +10,9 @@ run() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs pyt
 run c1 300 --config c1 --steps 5 --warmup 1
 run c2 400 --config c2 --steps 20 --warmup 3
 run c2l5 400 --config c2l5 --steps 20 --warmup 3
-run c2s8 200 --config c2 --steps 40 --warmup 5 --shard-of 8 --no-cpu-baseline
+run c2s8 200 --config c2 --steps 40 --warmup 5 --shard-of 8 --no-cpu-baseline --pmc profiles/pmc_c2s8.json
 run c3 400 --config c3 --steps 3 --warmup 1
+run c2i 300 --config c2i --steps 20 --warmup 5
 run c3g 400 --config c3g --steps 3 --warmup 1
 run c4 400 --config c4 --steps 5 --warmup 1
-run c5s8 300 --config c5 --steps 2 --warmup 1 --shard-of 8 --no-cpu-baseline
+run c5s8 300 --config c5 --steps 2 --warmup 1 --shard-of 8 --no-cpu-baseline --pmc profiles/pmc_c5s8.json
