@@ -113,11 +113,8 @@ typedef struct mrt_scene_info {
                                       the deeper tree.  ABI 7. */
   float occluder_cos_min;          /* shadow rays whose cosine to the target light's normal is below this
                                       traverse the main tree (bound on the light's own t error). ABI 7. */
-  /* ABI 8: the culled planes (n, w; inside n.x - w <= -occluder_margin) and
-   * the margin of nearest queries' exit bound: a ray reports no hit in a box
-   * it first enters beyond min over planes with n.d > 0 of
-   * (w - n.o + occluder_exit_margin) / (n.d) (the scene lies inside them). */
-  float occluder_exit_margin;
+  /* ABI 8: the culled planes (n, w; outward unit normal n, inside
+   * n.x - w <= -occluder_margin), occluder_planes of them */
   float occluder_plane[8][4];
 } mrt_scene_info;
 

@@ -774,7 +774,7 @@ __device__ __forceinline__ void primary_nearest(const DeviceScene& sc, const Lds
 
 template <int STACK, int MODE, bool ANY>
 __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
-                                         uint32_t target, int32_t root, float tbox = __builtin_inff()) {
+                                         uint32_t target, int32_t root) {
   const RayBox rb = make_raybox(o, d);
   int32_t node = root, leaf = 0;
   int sp = 0;
@@ -788,7 +788,7 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
     while (node != kDone && node >= 0) {
       LS_ADD(kLs + 2, 1);
       LS_ADD(kLs + 3, ls_lanes());
-      node = interior_step<STACK, MODE, ANY>(sc, cx, node, o, rb, tmin, ANY ? h.t : fminf(h.t, tbox), sp);
+      node = interior_step<STACK, MODE, ANY>(sc, cx, node, o, rb, tmin, h.t, sp);
       if (node < 0 && leaf == 0) {   // park the leaf, keep descending
         leaf = node;
         node = stack_pop<STACK>(cx, sp);
@@ -816,30 +816,6 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
 }
 
 
-// Exit bound of a nearest query (occluders.cpp): the scene lies inside every
-// culled plane, so no box entered beyond the first outward crossing
-// (w - n.o) / (n.d) plus the margin holds a triangle the ray can report.
-// The plane data is wave-uniform (kernel argument).  MRT_EXIT_CLAMP=0
-// compiles it out (A/B).
-#ifndef MRT_EXIT_CLAMP
-#define MRT_EXIT_CLAMP 1
-#endif
-__device__ __forceinline__ float exit_bound(const DeviceScene& sc, V3 o, V3 d) {
-  float tb = __builtin_inff();
-#if MRT_EXIT_CLAMP
-  for (uint32_t k = 0; k < sc.occ_planes; ++k) {
-    const float* p = sc.occ_plane[k];
-    const float c = fmaf(p[0], d.x, fmaf(p[1], d.y, p[2] * d.z));
-    const float num = (p[3] + sc.occ_exit_margin) - fmaf(p[0], o.x, fmaf(p[1], o.y, p[2] * o.z));
-    if (c > 0.0f) tb = fminf(tb, num / c);
-  }
-  tb = tb * 1.0001f;   // the division's and products' rounding (a few ulps)
-#else
-  (void)sc; (void)o; (void)d;
-#endif
-  return tb;
-}
-
 template <int STACK, int MODE>
 __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
                                              float tmax) {
@@ -848,7 +824,7 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
-  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u, sc.root, exit_bound(sc, o, d));
+  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u, sc.root);
   return h;
 }
 

@@ -122,11 +122,6 @@ struct DeviceScene {
   float occ_cos_min;         // ... and whose cosine to the target light's (interpolated) normal is at least
                              // this (grazing guard for the light's own t error, occluders.cpp)
   float occ_plane[8][4];
-  // nearest queries: every scene triangle lies inside each culled plane, so a
-  // ray reports no hit beyond the first plane it leaves through; boxes whose
-  // entry lies beyond (w - n.o + occ_exit_margin) / (n.d) are not visited
-  // (kernels.hip exit_bound; occluders.cpp for the margin)
-  float occ_exit_margin;
 };
 constexpr uint32_t kMaxOccPlanes = 8;
 // the origin-triangle early-out pays where a shadow ray's descent to its own

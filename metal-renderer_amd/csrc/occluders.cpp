@@ -29,19 +29,6 @@
 // already compute, so cos_min also adds twice the largest deviation of a
 // light vertex normal from its triangle's geometric normal (ANGLE below).
 // Rays under cos_min (a negligible share) traverse the main tree.
-//
-// Exit bound of nearest queries (kernels.hip exit_bound).  Every scene vertex
-// lies inside each supporting plane (n, w) up to tol, so every triangle lies in
-// the half-space n.x <= w + tol, and a ray that crosses the plane outward at
-// t_e = (w - n.o) / (n.d) is outside it, by (t - t_e) n.d, at every t > t_e.
-// A box the ray first enters beyond t_e + M / (n.d) is therefore passed at a
-// distance of more than M - tol from every triangle, beyond the slab test's
-// padding (bvh.cpp padded_box: 1e-5 |x| + 1e-6 per axis) when
-// M = 4 pad_max + tol + dev + 8 u S (dev: member planes against the group
-// plane; 8 u S: the float plane and the float evaluation of w - n.o): such a
-// box holds no triangle the leaf test can report for this ray, by the same
-// rule that makes the padded slab test exact, and skipping it changes no
-// answer.  The leaf tests keep h.t (no clamp on triangle acceptance).
 #include "occluders.h"
 
 #include <algorithm>
@@ -172,7 +159,6 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
   // the float plane differs from the double one by rounding: covered by the
   // runtime check's 8 u S term
   out.margin = (float)margin;
-  out.exit_margin = (float)(4.0 * (1e-5 * amax + 1e-6) + tol + dev_all + 8.0 * kUnit * S);
   // the grazing guard (header comment): D_L over the planes used, c_L and the
   // normal deviation over the light triangles
   double D_L = 1e300, c_L = 1.0, ndev = 0.0;

@@ -32,7 +32,6 @@ struct OccluderSet {
   float cos_min = 0.0f;                        // shadow rays with |cos| to the light's normal below this
                                                //   traverse the main tree (grazing guard, occluders.cpp)
   uint32_t culled = 0;                         // triangles left out
-  float exit_margin = 0.0f;                    // nearest-query exit bound's margin (occluders.cpp)
 };
 
 // positions: 3 floats per vertex at `stride_bytes`; light_vertices and

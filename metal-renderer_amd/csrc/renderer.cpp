@@ -205,7 +205,6 @@ struct mrt_renderer {
   std::unique_ptr<mrt::NoiseSchedule> noise;
   mrt::NoiseSchedule::Counters noise_base;   // the schedule's counters at the last stats reset
   uint64_t draw_seq = 0;     // draws enqueued (pins the noise chunks a draw reads)
-  uint64_t batch_seq = 0;    // frame batches enqueued (MRT_FLAG_PROFILE times every profile_every-th)
   uint64_t frame_index = 0;
   // Draws in flight: each draw records its survivor counters and events in
   // its own ring entry, and its statistics are read back lazily (when the
@@ -856,7 +855,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     in.occluder_margin = occ.margin;
     in.occluder_max_stack = ob.max_stack;
     in.occluder_cos_min = occ.cos_min;
-    in.occluder_exit_margin = occ.exit_margin;
     for (size_t k = 0; k < occ.planes.size() && k < 8; ++k)
       for (int c = 0; c < 4; ++c) in.occluder_plane[k][c] = occ.planes[k][c];
   }
@@ -918,7 +916,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     d.occ_planes = (uint32_t)occ.planes.size();
     d.occ_margin = occ.margin;
     d.occ_cos_min = occ.cos_min;
-    d.occ_exit_margin = occ.exit_margin;
     for (uint32_t k = 0; k < d.occ_planes; ++k)
       for (int c = 0; c < 4; ++c) d.occ_plane[k][c] = occ.planes[k][c];
     d.max_stack = std::max(d.max_stack, ob.max_stack);
@@ -1519,7 +1516,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.span = r->wall_khz > 0.0
                    ? reinterpret_cast<unsigned long long*>(static_cast<char*>(d.counters.p) + span_off) + 2 * k
                    : nullptr;
-      const bool timed = profile && (r->batch_seq % r->profile_every) == 0;
+      // every batch holding a frame f with f % profile_every == 0: every
+      // batch of a batched draw, every 8th single-frame draw
+      const bool timed = profile && ((f % r->profile_every) == 0 || (f % r->profile_every) + batch > r->profile_every);
       if (timed) HIP_TRY(hipEventRecord(d.kernel_events[ev++], fs.stream));
       if (r->path_mode) HIP_TRY(launch_paths(r, a, fs.stream));
       else if (r->stream_mode) HIP_TRY(launch_stream(r, a, fs.stream));
@@ -1555,7 +1554,6 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     HIP_TRY(launch_accumulate_frame(r, acc, r->stream));
     HIP_TRY(hipEventRecord(fs.acc_done, r->stream));
     fs.acc_recorded = true;
-    r->batch_seq += 1;
   }
   r->slot_next = (s0 + nb) % r->inflight;
   HIP_TRY(hipEventRecord(d.stop, r->stream));

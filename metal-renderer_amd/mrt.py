@@ -97,7 +97,7 @@ class SceneInfo(ctypes.Structure):
         ("occluder_planes", ctypes.c_uint32), ("occluder_culled", ctypes.c_uint32),
         ("occluder_nodes", ctypes.c_uint32), ("occluder_margin", ctypes.c_float),
         ("occluder_max_stack", ctypes.c_uint32), ("occluder_cos_min", ctypes.c_float),
-        ("occluder_exit_margin", ctypes.c_float), ("occluder_plane", (ctypes.c_float * 4) * 8),
+        ("occluder_plane", (ctypes.c_float * 4) * 8),
     ]
 
 

@@ -86,6 +86,11 @@ def test_occluder_planes_of_the_shipped_scenes(mrt_mod):
     assert s.info["occluder_culled"] == 14         # their 10 triangles + the two boxes' bottoms
     assert s.info["occluder_nodes"] >= 1
     assert 0 < s.info["occluder_margin"] < 1e-4    # below DISTANCE_EPSILON: origins on the walls qualify
+    # ABI 8 exports the planes: unit outward normals, every vertex inside
+    P = np.array(s.info["occluder_plane"][:5], np.float64)
+    assert np.allclose(np.linalg.norm(P[:, :3], axis=1), 1.0, atol=1e-6)
+    V = s.export()["vertices"]["v"].astype(np.float64)
+    assert (V @ P[:, :3].T - P[:, 3] <= 1e-5).all()
     off = mrt_mod.Scene("cornellbox", device=-1, occluder_tree=False)
     assert off.info["occluder_planes"] == 0 and off.info["occluder_culled"] == 0
     # Water scenes: the walls are < 1/8 of 7 K triangles: no second tree
