@@ -1433,7 +1433,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   const uint32_t launches_per_batch = r->path_mode || r->stream_mode ? 1u : L;
   const bool profile = (r->desc.flags & MRT_FLAG_PROFILE) != 0;
   if (profile) {
-    const size_t need = (size_t)2 * ((nb + r->profile_every - 1) / r->profile_every) * launches_per_batch;
+    const size_t need = (size_t)2 * nb * launches_per_batch;   // at most every batch is timed
     while (d.kernel_events.size() < need) {
       hipEvent_t e;
       HIP_TRY(hipEventCreate(&e));

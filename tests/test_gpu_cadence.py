@@ -116,3 +116,17 @@ def test_static_noise_per_frame(gpu, mrt_mod, box):
     assert _img(a) == _img(b)
     a.close()
     b.close()
+
+
+def test_profiled_draws_time_batches_holding_every_8th_frame(gpu, mrt_mod, box, monkeypatch):
+    """MRT_FLAG_PROFILE times (HIP events) every batch that holds a frame
+    f with f % 8 == 0: batches of 4 frames -> every other batch; single-frame
+    draws -> every 8th draw."""
+    monkeypatch.setenv("MRT_BATCH", "4")
+    r = mrt_mod.Renderer(box, 128, 96, 3, profile=True)
+    r.draw(20)                     # batches at frames 0, 4, 8, 12, 16: 0, 8, 16 timed
+    assert r.stats()["timed_launches"] == 3
+    for _ in range(16):            # frames 20..35: 24 and 32
+        r.draw_frame()
+    assert r.stats()["timed_launches"] == 5
+    r.close()
