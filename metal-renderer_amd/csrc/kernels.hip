@@ -772,115 +772,9 @@ __device__ __forceinline__ void primary_nearest(const DeviceScene& sc, const Lds
   }
 }
 
-// Cooperative leaf tests (VERDICT r4 item 2, A/B variant MRT_COOP_LEAF=1;
-// measured C2 -5.5 %, not kept): when the wave's pending leaf triangles —
-// each lane's parked leaf plus the next node when that is a leaf too — number
-// at most 64, they are spread one per lane over the wave through an LDS item
-// table; a helper pulls the owner's ray and h.t (ds_bpermute), runs tri_bary
-// and the acceptance rule, and the owner pulls the results back and merges
-// them in (t, prim) order.  Known defect of this variant: lanes masked off at
-// the call site are not helpers (the traversal would have to be called in
-// wave-uniform control flow).
-#ifndef MRT_COOP_LEAF
-#define MRT_COOP_LEAF 0
-#endif
-template <int STACK, int MODE, bool ANY>
-__device__ __forceinline__ bool traverse_coop(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
-                                              uint32_t target, int32_t root) {
-  const RayBox rb = make_raybox(o, d);
-  int32_t node = root, leaf = 0;
-  int sp = 0;
-  bool occluded = false;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  if (node < 0) { leaf = node; node = kDone; }
-  while (__ballot(node != kDone || leaf != 0)) {
-    while (node != kDone && node >= 0) {
-      node = interior_step<STACK, MODE, ANY>(sc, cx, node, o, rb, tmin, h.t, sp);
-      if (node < 0 && leaf == 0) { leaf = node; node = stack_pop<STACK>(cx, sp); }
-      if ((uint32_t)__popcll(__ballot(leaf == 0)) <= (uint32_t)MRT_TRAV_SLACK) break;
-    }
-    while (__ballot(leaf < 0)) {
-      const bool has = leaf < 0;
-      const bool chain = has && node < 0 && node != kDone;
-      const uint32_t lr0 = ~(uint32_t)leaf, lr1 = ~(uint32_t)node;
-      const uint32_t c0 = has ? (lr0 & (kMaxLeafSize - 1)) + 1 : 0u;
-      const uint32_t c1 = chain ? (lr1 & (kMaxLeafSize - 1)) + 1 : 0u;
-      const uint32_t w = c0 + c1;
-      const uint64_t B0 = __ballot(w & 1u), B1 = __ballot(w & 2u), B2 = __ballot(w & 4u);
-      const uint32_t total = (uint32_t)(__popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2));
-      if (total <= 64u && !__ballot(w > 4u)) {
-        const uint32_t base = (uint32_t)(__popcll(B0 & below) + 2 * __popcll(B1 & below) + 4 * __popcll(B2 & below));
-        __shared__ uint32_t s_items[kBlock];
-        uint32_t* items = s_items + (threadIdx.x & ~63u);
-        const uint32_t f0 = lr0 >> kLeafCountBits, f1 = lr1 >> kLeafCountBits;
-        for (uint32_t i = 0; i < w; ++i) items[base + i] = ((i < c0 ? f0 + i : f1 + (i - c0)) << 6) | lane;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const bool mine = lane < total;
-        const uint32_t item = mine ? items[lane] : 0u;
-        const uint32_t owner = mine ? (item & 63u) : lane;
-        const uint32_t k = item >> 6;
-        const V3 oo = mk(__shfl(o.x, owner), __shfl(o.y, owner), __shfl(o.z, owner));
-        const V3 od = mk(__shfl(d.x, owner), __shfl(d.y, owner), __shfl(d.z, owner));
-        const float ht = __shfl(h.t, owner);
-        float rt = __builtin_inff(), ru = 0.0f, rv = 0.0f;
-        uint32_t rp = 0xFFFFFFFFu;
-        bool hit = false;
-        if (mine) {
-          float4 t0, t1, t2;
-          fetch_tri<MODE>(sc, cx, k, t0, t1, t2);
-          float t, u, v;
-          const bool ok = tri_bary(oo, od, mk(t0), mk(t1), mk(t2), t, u, v);
-          const uint32_t prim = fbits(t0.w);
-          if (ANY) {
-            const uint32_t otgt = (uint32_t)__shfl((int)target, owner);
-            hit = ok & (t >= tmin) & (t <= ht) & (prim != otgt) & ((t < ht) | (prim < otgt));
-          } else {
-            hit = ok & (t >= tmin) & (t <= ht);
-          }
-          rt = t; ru = u; rv = v; rp = prim;
-        }
-        if (ANY) {
-          const uint64_t hm = __ballot(hit);
-          const uint64_t mask = w ? ((w == 4 ? 0xFull : ((1ull << w) - 1ull)) << base) : 0ull;
-          if (has && (hm & mask)) occluded = true;
-        } else {
-#pragma unroll
-          for (uint32_t i = 0; i < 4; ++i) {
-            const uint32_t src = base + min(i, 63u);
-            const bool hi = (uint32_t)__shfl((int)hit, src) != 0u;
-            const float ti = __shfl(rt, src), ui = __shfl(ru, src), vi = __shfl(rv, src);
-            const uint32_t pi = (uint32_t)__shfl((int)rp, src);
-            if (i < w && hi && (!h.found | (ti < h.t) | (pi < h.prim)) && ti <= h.t) {
-              h.found = true; h.t = ti; h.u = ui; h.v = vi; h.prim = pi;
-            }
-          }
-        }
-        if (has) {
-          leaf = 0;
-          if (chain) node = stack_pop<STACK>(cx, sp);
-          if (node < 0 && node != kDone) { leaf = node; node = stack_pop<STACK>(cx, sp); }
-          if (ANY && occluded) { leaf = 0; node = kDone; }
-        }
-      } else if (has) {
-        if (leaf_tests<MODE>(sc, cx, o, d, tmin, lr0 >> kLeafCountBits, c0, h, ANY, target, nullptr)) {
-          occluded = true; leaf = 0; node = kDone;
-        } else {
-          leaf = 0;
-          if (node < 0) { leaf = node; node = stack_pop<STACK>(cx, sp); }
-        }
-      }
-    }
-  }
-  return occluded;
-}
-
 template <int STACK, int MODE, bool ANY>
 __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin, Hit& h,
                                          uint32_t target, int32_t root) {
-  if (MRT_COOP_LEAF && MODE == kAllLds) return traverse_coop<STACK, MODE, ANY>(sc, cx, o, d, tmin, h, target, root);
   const RayBox rb = make_raybox(o, d);
   int32_t node = root, leaf = 0;
   int sp = 0;
