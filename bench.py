@@ -108,6 +108,8 @@ def parse():
     p.add_argument("--exchange-backend", default="rccl", choices=["rccl", "host"],
                    help="rccl: libmrt's RCCL collective (one process per GPU); host: packed tiles through host "
                         "memory and a gloo gather (rehearsal of the N>1 path with several ranks on one GPU)")
+    p.add_argument("--no-image-check", action="store_true",
+                   help="c2i: skip the bitwise check of the timed image against draw_n (profiling passes)")
     p.add_argument("--sweep-gpus", default="",
                    help="comma-separated GPU counts (e.g. 1,2,4,8): one job per N, one JSON line each")
     p.add_argument("--rank-timeout", type=float, default=1800.0,
@@ -673,7 +675,7 @@ def main():
         result["parity"] = par[0]
         if len(par) > 1:
             result["parity_precise"] = par[1]
-    if per_frame and rank == 0 and world == 1:
+    if per_frame and rank == 0 and world == 1 and not args.no_image_check:
         # the timed progressive image == the same frames drawn in 64-frame
         # batches (draw_n), bitwise
         total = int(st["frame_index"])

@@ -63,9 +63,14 @@ def main(tag="r1", cfg="c2"):
     timed_ns, timed_n = None, None
     trace_csv = os.path.join(src, "trace", "run_kernel_trace.csv")
     steps_file = os.path.join(src, "steps")
+    def steps_lps():
+        f = [int(x) for x in open(steps_file).read().split()]
+        return f[0] * (f[2] if len(f) > 2 else 1), f[1] * (f[2] if len(f) > 2 else 1)   # launches: timed, warm-up
+
     if os.path.exists(trace_csv) and os.path.exists(steps_file):
-        steps, warm = (int(x) for x in open(steps_file).read().split())
-        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace_csv))
+        steps, warm = steps_lps()
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in
+                sorted(csv.DictReader(open(trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
                 if r["Kernel_Name"] == bounce["Name"]]
         if len(durs) >= steps + warm:
             tail = durs[-steps:]
@@ -74,7 +79,7 @@ def main(tag="r1", cfg="c2"):
     period_ns = None
     trace2_csv = os.path.join(src, "trace2", "run_kernel_trace.csv")
     if os.path.exists(trace2_csv) and os.path.exists(steps_file):
-        steps, warm = (int(x) for x in open(steps_file).read().split())
+        steps, warm = steps_lps()
         ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace2_csv))
               if r["Kernel_Name"] == bounce["Name"]]
         ev.sort()

@@ -22,7 +22,9 @@ md5sum metal-renderer_amd/lib/libmrt.so | cut -d' ' -f1 > $OUT/lib.md5
 # launches (prof_summary.py drops the WARM warm-up launches) is the kernel's
 # time per launch on one render stream
 STEPS=${STEPS:-12}; WARM=${WARM:-2}
-echo "$STEPS $WARM" > $OUT/steps
+# LPS: hot-kernel launches per step (64 for c2i: one per drawn frame)
+LPS=${LPS:-1}
+echo "$STEPS $WARM $LPS" > $OUT/steps
 BENCH="python3 bench.py --config $CFG --steps $STEPS --warmup $WARM --no-cpu-baseline $*"
 set -o pipefail
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1; local rc=$?; tail -n 3 $OUT/$name.log; echo "== $name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
