@@ -326,9 +326,7 @@ __host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t node_f4
 }
 // both trees' nodes and leaf-triangle records (mrt_layout.h DeviceScene)
 __host__ __device__ inline uint32_t scene_nodes(const DeviceScene& sc) { return sc.num_nodes + sc.occ_nodes; }
-__host__ __device__ inline uint32_t scene_tri_records(const DeviceScene& sc) {
-  return sc.num_triangles + sc.occ_tris + sc.wall_tris;
-}
+__host__ __device__ inline uint32_t scene_tri_records(const DeviceScene& sc) { return sc.num_triangles + sc.occ_tris; }
 __host__ __device__ inline uint32_t lds_scene_float4s(int mode, const DeviceScene& sc) {
   return lds_scene_float4s(mode, node_float4s(sc.width), scene_nodes(sc), sc.lds_nodes, scene_tri_records(sc),
                            sc.num_triangles, sc.num_materials, sc.num_lights + 1);
@@ -818,22 +816,6 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
 }
 
 
-// Nearest queries from inside the room (all-in-LDS scenes with culled
-// planes, DeviceScene::wall_counts).  Every scene triangle lies inside each
-// culled plane, so a ray whose origin is inside all of them (by occ_margin)
-// and which first leaves through plane e can hit, among the culled
-// triangles, only e's: the others lie in planes it moves away from (crossed
-// behind the origin) or crosses beyond e, outside the room.  It tests e's
-// triangles (copies of their leaf records, the leaf test's arithmetic and tie
-// rule) and then traverses the occluder tree (every other triangle) with that
-// hit as the bound: the brute-force answer, without walking the walls'
-// nodes and leaves.  Rays that graze a culled plane (|cos| < kWallCosMin) or
-// whose second crossing lies within 1 % (wall_tie) of the first traverse the
-// main tree (occluders.cpp bounds what float rounding could do in those).
-// MRT_WALL_NEAREST=0 compiles it out.
-#ifndef MRT_WALL_NEAREST
-#define MRT_WALL_NEAREST 1
-#endif
 template <int STACK, int MODE>
 __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
                                              float tmax) {
@@ -842,53 +824,7 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
-  int32_t root = sc.root;
-  if (MRT_WALL_NEAREST && MODE == kAllLds && sc.wall_counts) {   // wave-uniform
-    // planes to test: the exit plane, planes crossed within the tie window
-    // after it, planes the ray approaches at a grazing angle, and every plane
-    // it approaches when it grazes the exit plane; a ray almost parallel to a
-    // plane it leaves, or starting within the margin, takes the main tree
-    bool ok = true;
-    float te = __builtin_inff(), ce = 1.0f;
-    uint32_t toward = 0u, graze = 0u;
-    float tk[kMaxOccPlanes];
-#pragma unroll
-    for (uint32_t k = 0; k < kMaxOccPlanes; ++k) {
-      tk[k] = __builtin_inff();
-      if (k < sc.occ_planes) {
-        const float* p = sc.occ_plane[k];
-        const float dist = fmaf(p[0], o.x, fmaf(p[1], o.y, fmaf(p[2], o.z, -p[3])));   // n.o - w
-        const float c = fmaf(p[0], d.x, fmaf(p[1], d.y, p[2] * d.z));
-        ok &= (dist <= -sc.occ_margin) & ((c > 0.0f) | (c <= -1e-5f));
-        if (c > 0.0f) {
-          const float t = -dist * m_rcp(c);
-          tk[k] = t;
-          toward |= 1u << k;
-          if (c < kWallCosMin) graze |= 1u << k;
-          if (t < te) { te = t; ce = c; }
-        }
-      }
-    }
-    if (ok) {
-      uint32_t mask = graze | (ce < kWallCosMin ? toward : 0u);
-      const float win = te * 1.01f + sc.wall_tie;
-#pragma unroll
-      for (uint32_t k = 0; k < kMaxOccPlanes; ++k) mask |= ((toward >> k) & 1u) && tk[k] <= win ? 1u << k : 0u;   // the exit plane included
-      root = sc.occ_root;
-      const uint32_t base = sc.num_triangles + sc.occ_tris;
-      while (mask) {
-        const uint32_t k = __builtin_ctz(mask);
-        mask &= mask - 1u;
-        const uint32_t off = (uint32_t)((sc.wall_offs >> (8 * k)) & 0xFFull);
-        const uint32_t cnt = (sc.wall_counts >> (4 * k)) & 15u;
-        for (uint32_t i = 0; i < cnt; i += 2) {
-          const uint32_t i1 = min(i + 1, cnt - 1);
-          tri_pair<MODE>(sc, cx, o, d, tmin, base + off + i, base + off + i1, i1 != i, h, false, 0u, nullptr);
-        }
-      }
-    }
-  }
-  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u, root);
+  traverse<STACK, MODE, false>(sc, cx, o, d, tmin, h, 0u, sc.root);
   return h;
 }
 

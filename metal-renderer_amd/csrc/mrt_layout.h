@@ -122,24 +122,7 @@ struct DeviceScene {
   float occ_cos_min;         // ... and whose cosine to the target light's (interpolated) normal is at least
                              // this (grazing guard for the light's own t error, occluders.cpp)
   float occ_plane[8][4];
-  // nearest queries from inside every culled plane (kernels.hip
-  // trace_nearest_room): the culled triangles of each plane, copies of their
-  // main-tree leaf records, follow the occluder tree's records — plane k's
-  // (wall_counts >> 4k) & 15 of them, in plane order; wall_counts == 0: off.
-  // A ray whose first outward crossing is plane e tests e's records and then
-  // the occluder tree; wall_tie (scene units) and kWallCosMin bound the
-  // cases that fall back to the main tree (occluders.cpp).
-  uint32_t wall_counts;
-  uint32_t wall_tris;
-  float wall_tie;
-  uint64_t wall_offs;        // plane k's first record (relative) at bits [8k, 8k + 8)
 };
-// |cosine| of a nearest ray to every culled plane below which it traverses
-// the main tree (occluders.cpp: with near ties within 1 % of the scene scale
-// excluded, a culled triangle of a plane other than the exit plane cannot
-// report a hit for such a ray when c_max < kWallCMax)
-constexpr float kWallCosMin = 0.02f;
-constexpr double kWallCMax = 4.0;
 constexpr uint32_t kMaxOccPlanes = 8;
 // the origin-triangle early-out pays where a shadow ray's descent to its own
 // leaf goes through global memory: measured C4 (1M triangles) +2.6 %, C3

@@ -151,10 +151,7 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
   for (const Plane& P : used) {
     for (uint32_t t : P.tris) culled[t] = 1;
     out.planes.push_back({(float)P.n.x, (float)P.n.y, (float)P.n.z, (float)P.w});
-    out.plane_tris.push_back(P.tris);
-    out.c_max = std::max(out.c_max, P.c_max);
   }
-  out.scale = S;
   for (uint32_t t = 0; t < num_triangles; ++t) {
     if (culled[t]) ++out.culled;
     else out.keep.push_back(t);

@@ -32,9 +32,6 @@ struct OccluderSet {
   float cos_min = 0.0f;                        // shadow rays with |cos| to the light's normal below this
                                                //   traverse the main tree (grazing guard, occluders.cpp)
   uint32_t culled = 0;                         // triangles left out
-  std::vector<std::vector<uint32_t>> plane_tris;   // per entry of `planes`: its triangles (scene order)
-  double c_max = 1.0;                          // worst |e1||e2| / |e1 x e2| of the culled triangles
-  double scale = 0.0;                          // scene scale S (occluders.cpp)
 };
 
 // positions: 3 floats per vertex at `stride_bytes`; light_vertices and

@@ -108,9 +108,6 @@ struct mrt_scene {
   std::vector<uint32_t> occ_keep;   // primitives the occluder tree holds
   int32_t occ_root = 0;
   uint32_t occ_node_base = 0, occ_max_stack = 0;
-  uint32_t wall_counts = 0, wall_tris = 0;   // DeviceScene::wall_* (trace_nearest_room)
-  uint64_t wall_offs = 0;
-  float wall_tie = 0.0f;
   DevBuf nodes, tris, prims, materials, lights;
   mrt::DeviceScene dev{};
   mrt_scene_info info{};
@@ -848,26 +845,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
       s->occ_root = occ_root;
       s->occ_node_base = node_base;
       s->occ_max_stack = ob.max_stack;
-      // the culled planes' triangles for nearest queries (trace_nearest_room):
-      // copies of their main-tree leaf records, plane by plane, after the
-      // occluder tree's (at most 15 per plane, 4-bit counts)
-      bool walls = occ.c_max < mrt::kWallCMax;
-      for (const auto& pt : occ.plane_tris) walls = walls && pt.size() <= 15;
-      if (const char* v = std::getenv("MRT_WALLS")) walls = walls && std::atoi(v) != 0;
-      if (walls) {
-        std::vector<uint32_t> rec_of(T, 0xFFFFFFFFu);
-        for (uint32_t i = 0; i < T; ++i) rec_of[fbits(s->bvh.tris[12 * (size_t)i + 3])] = i;
-        for (size_t k = 0; k < occ.plane_tris.size(); ++k) {
-          for (uint32_t prim : occ.plane_tris[k]) {
-            const size_t r = rec_of[prim];
-            up_tris.insert(up_tris.end(), s->bvh.tris.begin() + 12 * r, s->bvh.tris.begin() + 12 * r + 12);
-          }
-          s->wall_offs |= (uint64_t)s->wall_tris << (8 * k);
-          s->wall_counts |= (uint32_t)occ.plane_tris[k].size() << (4 * k);
-          s->wall_tris += (uint32_t)occ.plane_tris[k].size();
-        }
-        s->wall_tie = (float)(0.01 * occ.scale);
-      }
     }
   }
   mrt_scene_info& in = s->info;
@@ -942,10 +919,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     for (uint32_t k = 0; k < d.occ_planes; ++k)
       for (int c = 0; c < 4; ++c) d.occ_plane[k][c] = occ.planes[k][c];
     d.max_stack = std::max(d.max_stack, ob.max_stack);
-    d.wall_counts = s->wall_counts;
-    d.wall_tris = s->wall_tris;
-    d.wall_tie = s->wall_tie;
-    d.wall_offs = s->wall_offs;
   }
   HIP_TRY(alloc_isect_spill(s->isect_spill, d.max_stack));
   in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
