@@ -108,6 +108,9 @@ def parse():
     p.add_argument("--exchange-backend", default="rccl", choices=["rccl", "host"],
                    help="rccl: libmrt's RCCL collective (one process per GPU); host: packed tiles through host "
                         "memory and a gloo gather (rehearsal of the N>1 path with several ranks on one GPU)")
+    p.add_argument("--sustain", type=float, default=3.0,
+                   help="N=1 batched configs: after the timed steps, keep stepping for this many seconds and "
+                        "report the sustained rate beside the line (0 = off; not the headline value)")
     p.add_argument("--no-image-check", action="store_true",
                    help="c2i: skip the bitwise check of the timed image against draw_n (profiling passes)")
     p.add_argument("--sweep-gpus", default="",
@@ -520,6 +523,25 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = r.stats()
+    sustained = None
+    if world == 1 and args.sustain > 0 and not per_frame:
+        # a longer window of the same steps (~seconds, visible to an outside
+        # utilisation sampler); the headline value stays the K timed steps
+        n_s, t_s = 0, time.perf_counter()
+        while True:
+            step()
+            n_s += 1
+            if n_s % 10 == 0:
+                r.sync()
+                if time.perf_counter() - t_s >= args.sustain:
+                    break
+        r.sync()
+        dt_s = time.perf_counter() - t_s
+        sustained = {"steps": n_s, "seconds": round(dt_s, 3),
+                     "value": round((st["paths"] - base["paths"]) / max(1, args.steps) * n_s / dt_s / 1e6, 3),
+                     "ms_per_step": round(dt_s / n_s * 1e3, 3),
+                     "note": "the same step repeated for --sustain seconds after the timed region (reported "
+                             "beside the line; value is the K timed steps)"}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -639,6 +661,8 @@ def main():
         "noise_ms_per_frame": noise["noise_ms_per_frame"],
         "noise": noise,
     }
+    if sustained:
+        result["sustained"] = sustained
     if per_frame:
         result["cadence"] = {
             "draw_calls": int(st["draws"] - base["draws"]),
