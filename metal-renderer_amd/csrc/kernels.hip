@@ -91,21 +91,40 @@ __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); 
 // ---------------------------------------------------------------------------
 // Moller-Trumbore, cull none; (u, v) are the weights of (V0, V1) as
 // interpolate() expects (renderer/KernelHelpers.h:37-47).
+// The triangle test's products and sums without FMA contraction
+// (MRT_TRI_NOCONTRACT): the same rounding in every inlined copy of the test —
+// with contraction the compiler may fuse differently per copy, and which copy
+// tests a triangle can depend on how a wave's traversal rounds fall
+#ifndef MRT_TRI_NOCONTRACT
+#define MRT_TRI_NOCONTRACT 0
+#endif
+__device__ __forceinline__ float tdot(V3 a, V3 b) {
+#if MRT_TRI_NOCONTRACT
+#pragma clang fp contract(off)
+#endif
+  return (a.x * b.x + a.y * b.y) + a.z * b.z;
+}
+__device__ __forceinline__ V3 tcross(V3 a, V3 b) {
+#if MRT_TRI_NOCONTRACT
+#pragma clang fp contract(off)
+#endif
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
 __device__ __forceinline__ bool tri_test(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float tmin, float tmax, float& t,
                                          float& u, float& v) {
   // early exits: most candidate triangles fail the first barycentric test,
   // and a wave whose lanes all fail skips the rest (s_cbranch_execz)
-  const V3 p = cross(d, e2);
-  const float det = dot(e1, p);
+  const V3 p = tcross(d, e2);
+  const float det = tdot(e1, p);
   if (det == 0.0f) return false;
   const float inv = m_rcp(det);
   const V3 s = sub(o, v0);
-  const float b1 = dot(s, p) * inv;
+  const float b1 = tdot(s, p) * inv;
   if (!(b1 >= 0.0f && b1 <= 1.0f)) return false;
-  const V3 q = cross(s, e1);
-  const float b2 = dot(d, q) * inv;
+  const V3 q = tcross(s, e1);
+  const float b2 = tdot(d, q) * inv;
   if (!(b2 >= 0.0f && b1 + b2 <= 1.0f)) return false;
-  const float tt = dot(e2, q) * inv;
+  const float tt = tdot(e2, q) * inv;
   if (!(tt >= tmin && tt <= tmax)) return false;
   t = tt;
   u = (1.0f - b1) - b2;
@@ -119,14 +138,14 @@ __device__ __forceinline__ bool tri_test(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float 
 // a triangle are all in flight together instead of v0's being issued only
 // after the determinant test passed.
 __device__ __forceinline__ bool tri_bary(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, float& v) {
-  const V3 p = cross(d, e2);
-  const float det = dot(e1, p);
+  const V3 p = tcross(d, e2);
+  const float det = tdot(e1, p);
   const float inv = m_rcp(det);
   const V3 s = sub(o, v0);
-  const float b1 = dot(s, p) * inv;
-  const V3 q = cross(s, e1);
-  const float b2 = dot(d, q) * inv;
-  t = dot(e2, q) * inv;
+  const float b1 = tdot(s, p) * inv;
+  const V3 q = tcross(s, e1);
+  const float b2 = tdot(d, q) * inv;
+  t = tdot(e2, q) * inv;
   u = (1.0f - b1) - b2;
   v = b1;
   return (det != 0.0f) & (b1 >= 0.0f) & (b1 <= 1.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f);
