@@ -89,7 +89,9 @@ struct BounceArgs {
   uint32_t debug;              // ablation bits for profiling (0 in production, env MRT_DEBUG):
                                //   1 = skip shadow traversal, 2 = skip shading, 4 = no queue writes,
                                //   8 = static interleaved work assignment (no grab counters),
-                               //   16 = no material partition of the survivors
+                               //   16 = no material partition of the survivors, 32 = no occlusion traversal
+                               //   of light samples, 64 = no occlusion query of last-bounce light hits,
+                               //   128 = no origin-triangle test (stream / bounce kernels)
   // segmented queues: block g of a launch appends its class-0 survivors
   // (left a diffuse surface) to [g*cap, g*cap + c0_g) and its class-1
   // survivors to [g*cap + cap - c1_g, g*cap + cap) of the output queue

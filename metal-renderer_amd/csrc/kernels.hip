@@ -863,13 +863,39 @@ __device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o, bool
   return inside ? sc.occ_root : sc.root;
 }
 
+// The light triangles of an occluder tree built without them (DeviceScene::
+// occ_lights): every shadow ray enters the light's own leaf box, so instead
+// of a leaf visit per ray the other light triangles are tested here in one
+// wave-uniform loop — the leaf test's arithmetic (a light record's vertices
+// are its primitive's, in its order: v2 - v1, v3 - v1 are the leaf record's
+// e1, e2 bit for bit, as in last_bounce_light_hit) and the occlusion rule
+// (k != target, (t_k, k) < (t_T, target), t_k >= 0), so the query's answer
+// is unchanged.
+template <int MODE>
+__device__ __forceinline__ bool lights_occlude(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
+                                               float tT) {
+  bool occ = false;
+  for (uint32_t k = 0; k < sc.num_lights; ++k) {   // wave-uniform
+    const float4 LB = fetch_light<MODE>(sc, cx, k, 1), LD = fetch_light<MODE>(sc, cx, k, 3);
+    const float4 LF = fetch_light<MODE>(sc, cx, k, 5);
+    const uint32_t prim = fbits(LD.w);
+    const V3 p0 = mk(LB);
+    float t, u, v;
+    const bool ok = tri_bary(o, d, p0, sub(mk(LD), p0), sub(mk(LF), p0), t, u, v);
+    occ |= ok & (prim != target) & (t >= 0.0f) & (t <= tT) & ((t < tT) | (prim < target));
+  }
+  return occ;
+}
+
 template <int STACK, int MODE>
 __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
                                                float t_target, bool graze) {
   Hit h;
   h.t = t_target;
   h.found = false;
-  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, shadow_root(sc, o, graze));
+  const int32_t root = shadow_root(sc, o, graze);
+  if (sc.occ_lights && root == sc.occ_root && lights_occlude<MODE>(sc, cx, o, d, target, t_target)) return true;
+  return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, root);
 }
 
 // The shadow ray's own surface first (exact early-out, r4).  The occlusion
@@ -890,6 +916,11 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
 // (DeviceScene::origin_test; MRT_ORIGIN_TEST=0 compiles it out).
 #ifndef MRT_ORIGIN_TEST
 #define MRT_ORIGIN_TEST 1
+#endif
+// the last bounce's occlusion query of a light hit through the occluder tree
+// (shadow_root) instead of the main tree
+#ifndef MRT_LAST_OCC
+#define MRT_LAST_OCC 1
 #endif
 template <int MODE>
 __device__ __forceinline__ bool origin_occludes(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t prim,
@@ -913,13 +944,14 @@ __device__ __forceinline__ bool origin_occludes(const DeviceScene& sc, const Lds
 // `origin` = the primitive the ray leaves (origin_occludes).
 template <int STACK, int MODE>
 __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                                      uint32_t origin, bool graze) {
+                                      uint32_t origin, bool graze, uint32_t dbg = 0u) {
   const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
   float tT, u, v;
   if (!tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v)) return false;
   if (!(tT >= kDistanceEpsilon)) return false;
-  if (origin_occludes<MODE>(sc, cx, o, d, origin, target, tT)) return false;
+  if (!(dbg & 128u) && origin_occludes<MODE>(sc, cx, o, d, origin, target, tT)) return false;
+  if (dbg & 32u) return true;   // ablation: no occlusion traversal
   return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT, graze);
 }
 
@@ -941,12 +973,17 @@ __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V
 // Measured (r4, alternating in one call): C2 (stream kernel) 9738 / 9743 ->
 // 10772 / 10778 Mpaths/s (+10.6 %); the path kernel keeps the full query
 // (MRT_PATH_LAST_LIGHT).
+// `graze`: the hit light's cosine to the ray is below the occluder tree's
+// guard (shadow_root; |d . n| / |n| over the geometric normal n = e1 x e2,
+// which occluders.cpp's cos_min covers as it covers the interpolated normal).
 template <int MODE>
-__device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, Hit& h) {
+__device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, Hit& h,
+                                                      bool& graze) {
   h.t = __builtin_inff();
   h.u = h.v = 0.0f;
   h.prim = 0xFFFFFFFFu;
   h.found = false;
+  float gd = 0.0f, gn = 1.0f;   // the nearest light's (d . n)^2 and n . n
   for (uint32_t k = 0; k < sc.num_lights; ++k) {   // wave-uniform
     // the light record's vertices are the primitive's, in its order
     // (scene flattening, Renderer.mm:394-413): three independent loads, and
@@ -954,9 +991,9 @@ __device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, con
     const float4 LB = fetch_light<MODE>(sc, cx, k, 1), LD = fetch_light<MODE>(sc, cx, k, 3);
     const float4 LF = fetch_light<MODE>(sc, cx, k, 5);
     const uint32_t prim = fbits(LD.w);   // lights[k].index
-    const V3 p0 = mk(LB), p1 = mk(LD), p2 = mk(LF);
+    const V3 p0 = mk(LB), e1 = sub(mk(LD), p0), e2 = sub(mk(LF), p0);
     float t, u, v;
-    const bool ok = tri_bary(o, d, p0, sub(p1, p0), sub(p2, p0), t, u, v);
+    const bool ok = tri_bary(o, d, p0, e1, e2, t, u, v);
     const bool hit = ok & (t >= 0.0f) & (t <= h.t);
     if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
       h.found = true;
@@ -964,9 +1001,14 @@ __device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, con
       h.u = u;
       h.v = v;
       h.prim = prim;
+      const V3 n = tcross(e1, e2);
+      const float dn = tdot(d, n);
+      gd = dn * dn;
+      gn = tdot(n, n);
     }
   }
   if (h.found && h.t < kDistanceEpsilon) h.found = false;   // no emission whatever is nearer
+  graze = !(gd >= (sc.occ_cos_min * sc.occ_cos_min) * gn);
   return h.found;
 }
 
@@ -1500,11 +1542,16 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   if (active && !listed) {
     if (last && sc.light_shortcut && !(a.flags & kShadeDebugMaterial)) {
       // the last bounce: light triangles, then one occlusion query (last_bounce_light_hit)
-      if (last_bounce_light_hit<MODE>(sc, cx, s.o, s.d, h)) {
+      bool graze;
+      if (last_bounce_light_hit<MODE>(sc, cx, s.o, s.d, h, graze)) {
+        // the light hit is the target of a shadow query from s.o: the
+        // occluder tree when shadow_root allows it (the other lights lost to
+        // it in last_bounce_light_hit already, so no lights_occlude here)
         Hit hh;
         hh.t = h.t;
         hh.found = false;
-        if (traverse<STACK, MODE, true>(sc, cx, s.o, s.d, 0.0f, hh, h.prim, sc.root)) h.found = false;
+        const int32_t root = MRT_LAST_OCC ? shadow_root(sc, s.o, graze) : sc.root;
+        if (!(a.debug & 64u) && traverse<STACK, MODE, true>(sc, cx, s.o, s.d, 0.0f, hh, h.prim, root)) h.found = false;
       }
     } else {
       h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
@@ -1588,7 +1635,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
     LS_ADD(16, (uint32_t)__popcll(__ballot(sh.valid)));
     LS_ADD(17, 1);
   }
-  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target, h.prim, sh.graze))) {
+  if (sh.valid && ((a.debug & 1u) || shadow_reaches_target<STACK, MODE>(sc, cx, sh.o, sh.d, sh.target, h.prim, sh.graze, a.debug))) {
     s.R = add(s.R, sh.L);
   }
   if (alive && !(a.debug & 4u)) out_q.plane[3][o] = make_float4(s.R.x, s.R.y, s.R.z, s.ior);
@@ -1965,11 +2012,12 @@ __device__ __forceinline__ void begin_nearest(const DeviceScene& sc, const LdsCt
                                               V3 ro, V3 rd, Hit& h, Trav& tr, uint32_t& phase, uint32_t& target,
                                               bool& occluded) {
   if (last && shortcut) {
-    if (last_bounce_light_hit<MODE>(sc, cx, ro, rd, h)) {
+    bool graze;
+    if (last_bounce_light_hit<MODE>(sc, cx, ro, rd, h, graze)) {
       phase = 3;
       target = h.prim;
       occluded = false;
-      trav_begin(sc.root, tr);
+      trav_begin(MRT_LAST_OCC ? shadow_root(sc, ro, graze) : sc.root, tr);
     } else {
       phase = 1;
       tr.node = kDone;
@@ -2180,12 +2228,14 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
           const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
           const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
           float tT, u, v;
+          const int32_t sroot = shadow_root(sc, ro, sh.graze);
           if (tri_test(ro, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
-              !(tT < kDistanceEpsilon) && !origin_occludes<MODE>(sc, cx, ro, sh.d, h.prim, sh.target, tT)) {
+              !(tT < kDistanceEpsilon) && !origin_occludes<MODE>(sc, cx, ro, sh.d, h.prim, sh.target, tT) &&
+              !(sc.occ_lights && sroot == sc.occ_root && lights_occlude<MODE>(sc, cx, ro, sh.d, sh.target, tT))) {
             shadow = true;
             phase = 2;
             rd = sh.d;   // ro = s.o = sh.o
-            trav_begin(shadow_root(sc, ro, sh.graze), tr);
+            trav_begin(sroot, tr);
             h.t = tT;
             h.u = sh.L.x;
             h.v = sh.L.y;

@@ -118,6 +118,8 @@ struct DeviceScene {
   uint32_t occ_nodes;
   uint32_t occ_tris;
   uint32_t occ_planes;
+  uint32_t occ_lights;       // the occluder tree holds no light triangle: queries through it test the
+                             // other light triangles in a loop instead (kernels.hip lights_occlude)
   float occ_margin;
   float occ_cos_min;         // ... and whose cosine to the target light's (interpolated) normal is at least
                              // this (grazing guard for the light's own t error, occluders.cpp)
@@ -138,6 +140,9 @@ constexpr uint32_t kRegionGrabTriangles = 65536;
 constexpr uint32_t kGreedyCollapseTriangles = 65536;
 // light triangles tested per last-bounce ray by last_bounce_light_hit
 constexpr uint32_t kLightShortcutMax = 16;
+// occluder trees leave the light triangles out (tested in a loop per
+// occlusion query, kernels.hip lights_occlude) up to this many lights
+constexpr uint32_t kOccLightsMax = 8;
 
 // camera-ray candidate lists (primary.h): header (offset << 8) | count per
 // 8x8 pixel block; count kPrimaryFallback = traverse the BVH

@@ -802,6 +802,19 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     occ_on = mrt::find_occluders(h.vertices.data()->v, sizeof(mrt::RefVertex), (uint32_t)h.vertices.size(),
                                  h.indices.data(), T, lv.data(), ln.data(), h.light_count, occ);
   }
+  // with few light triangles the occluder tree leaves them out: every shadow
+  // ray enters the light's own leaf box, and the kernels test the other
+  // light triangles in one wave-uniform loop instead (kernels.hip
+  // lights_occlude; MRT_OCC_LIGHTS=0 keeps them in the tree)
+  bool occ_lights = occ_on && h.light_count <= mrt::kOccLightsMax;
+  if (const char* v = std::getenv("MRT_OCC_LIGHTS")) occ_lights = occ_lights && std::atoi(v) != 0;
+  if (occ_lights) {
+    std::vector<uint8_t> is_light(T, 0);
+    for (uint32_t l = 0; l < h.light_count; ++l)
+      if (h.lights[l].index < T) is_light[h.lights[l].index] = 1;
+    occ.keep.erase(std::remove_if(occ.keep.begin(), occ.keep.end(), [&](uint32_t t) { return is_light[t] != 0; }),
+                   occ.keep.end());
+  }
   const uint32_t node_base = (uint32_t)(s->bvh.nodes.size() / 32), tri_base = T;
   int32_t occ_root = mrt::kEmptyChild;
   if (occ_on && !occ.keep.empty()) {
@@ -810,6 +823,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     for (uint32_t t : occ.keep) sub.insert(sub.end(), {h.indices[3 * t], h.indices[3 * t + 1], h.indices[3 * t + 2]});
     mrt::BvhBuildOptions oo = opt;
     oo.lds_node_budget = 0;
+    if (const char* v = std::getenv("MRT_OCC_LEAF"))
+      oo.max_leaf_size = std::max(1u, std::min<uint32_t>(mrt::kMaxLeafSize, (uint32_t)std::strtoul(v, nullptr, 0)));
+    if (const char* v = std::getenv("MRT_OCC_TCOST")) oo.traversal_cost = std::strtof(v, nullptr);
     if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), sub.data(), (uint32_t)occ.keep.size(), oo, ob, err))
       return fail(MRT_ERR_INVALID, "occluder BVH build failed: " + err);
     auto rebase = [&](int32_t r) -> int32_t {
@@ -910,7 +926,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (const char* v = std::getenv("MRT_LAST_LIGHT")) d.light_shortcut = d.light_shortcut && std::atoi(v) != 0;
   d.occ_root = occ_root;
   d.occ_planes = 0;
+  d.occ_lights = 0;
   if (occ_on) {
+    d.occ_lights = occ_lights ? 1u : 0u;
     d.occ_nodes = (uint32_t)(up_nodes.size() / 32) - s->bvh.num_nodes;   // (a leaf-root main tree keeps one dummy node)
     d.occ_tris = (uint32_t)occ.keep.size();
     d.occ_planes = (uint32_t)occ.planes.size();
