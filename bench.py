@@ -81,8 +81,10 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=None,
+                   help="timed steps (default: 100 for c2 / c2l5, whose step is ~12 ms, so the timed region is "
+                        "over a second; 5 otherwise)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 5 for c2 / c2l5, 1 otherwise)")
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--max-path-length", type=int, default=0,
                    help="override the config's MAX_PATH_LENGTH (e.g. 5 = primary ray + 4 bounces)")
@@ -108,7 +110,7 @@ def parse():
     p.add_argument("--exchange-backend", default="rccl", choices=["rccl", "host"],
                    help="rccl: libmrt's RCCL collective (one process per GPU); host: packed tiles through host "
                         "memory and a gloo gather (rehearsal of the N>1 path with several ranks on one GPU)")
-    p.add_argument("--sustain", type=float, default=3.0,
+    p.add_argument("--sustain", type=float, default=10.0,
                    help="N=1 batched configs: after the timed steps, keep stepping for this many seconds and "
                         "report the sustained rate beside the line (0 = off; not the headline value)")
     p.add_argument("--no-image-check", action="store_true",
@@ -117,7 +119,13 @@ def parse():
                    help="comma-separated GPU counts (e.g. 1,2,4,8): one job per N, one JSON line each")
     p.add_argument("--rank-timeout", type=float, default=1800.0,
                    help="self-launched ranks: seconds before a job whose ranks have not all exited is killed")
-    return p.parse_args()
+    args = p.parse_args()
+    long_default = args.config in ("c2", "c2l5")
+    if args.steps is None:
+        args.steps = 100 if long_default else 5
+    if args.warmup is None:
+        args.warmup = 5 if long_default else 1
+    return args
 
 
 def _child_argv(n):

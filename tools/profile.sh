@@ -25,7 +25,7 @@ STEPS=${STEPS:-12}; WARM=${WARM:-2}
 # LPS: hot-kernel launches per step (64 for c2i: one per drawn frame)
 LPS=${LPS:-1}
 echo "$STEPS $WARM $LPS" > $OUT/steps
-BENCH="python3 bench.py --config $CFG --steps $STEPS --warmup $WARM --no-cpu-baseline $*"
+BENCH="python3 bench.py --config $CFG --steps $STEPS --warmup $WARM --no-cpu-baseline --sustain 0 $*"
 set -o pipefail
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1; local rc=$?; tail -n 3 $OUT/$name.log; echo "== $name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -f csv -- $BENCH
