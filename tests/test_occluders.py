@@ -80,6 +80,23 @@ def _tri_t(o, d, v0, e1, e2, fma):
     return t, ok
 
 
+@pytest.mark.parametrize("scene", ["cornellbox", "white-box"])
+@pytest.mark.parametrize("lights_out", ["1", "0"])
+def test_occluder_tree_with_and_without_lights_checks(mrt_mod, monkeypatch, scene, lights_out):
+    """The occluder tree with the light triangles left out (the default; the
+    kernels test them in lights_occlude) or kept (MRT_OCC_LIGHTS=0) passes
+    the host tree check: exactly the kept primitives, boxes containing them,
+    its stack bound.  white-box keeps only its two light triangles, so with
+    them out there is no tree at all (occ_root = kEmptyChild)."""
+    monkeypatch.setenv("MRT_OCC_LIGHTS", lights_out)
+    s = mrt_mod.Scene(scene, device=-1)
+    assert s.info["occluder_planes"] == 5
+    s.check_bvh()
+    if scene == "white-box":
+        assert s.info["occluder_culled"] == 10 and s.info["occluder_nodes"] == 0
+    s.close()
+
+
 def test_occluder_planes_of_the_shipped_scenes(mrt_mod):
     s = mrt_mod.Scene("cornellbox", device=-1)
     assert s.info["occluder_planes"] == 5          # floor, ceiling, back, left, right walls
@@ -268,12 +285,15 @@ def test_sliver_light_grazing_rays_never_culled_hits(mrt_mod, tmp_path, fma):
 def test_gpu_occluder_tree_renders_bitwise(gpu, mrt_mod, monkeypatch, kernel, precise, scene, W, H, L):
     """Shadow rays through the occluder tree give the same answers as through
     the whole scene: images and ray counts bitwise equal with the tree on and
-    off, in every kernel (stream, per-bounce, path) and both builds."""
+    off, in every kernel (stream, per-bounce, path) and both builds — and with
+    the light triangles left out of the tree (tested in lights_occlude, the
+    default) or kept in it (MRT_OCC_LIGHTS=0)."""
     monkeypatch.setenv("MRT_STREAM", "0" if kernel == "bounce" else "1")
     if kernel == "path":
         monkeypatch.setenv("MRT_KERNEL", "path")
     out = []
-    for tree in (True, False):
+    for tree, lights_out in ((True, True), (True, False), (False, True)):
+        monkeypatch.setenv("MRT_OCC_LIGHTS", "1" if lights_out else "0")
         s = mrt_mod.Scene(scene, occluder_tree=tree)
         assert (s.info["occluder_planes"] > 0) == tree
         r = mrt_mod.Renderer(s, W, H, L, precise=precise)
@@ -281,6 +301,7 @@ def test_gpu_occluder_tree_renders_bitwise(gpu, mrt_mod, monkeypatch, kernel, pr
         out.append((r.read_image(), r.stats()["active_ray_bounces"]))
         r.close()
         s.close()
-    (a, na), (b, nb) = out
+    (a, na) = out[0]
     assert np.isfinite(a).all() and a[..., :3].max() > 0
-    assert a.tobytes() == b.tobytes() and na == nb
+    for b, nb in out[1:]:
+        assert a.tobytes() == b.tobytes() and na == nb
