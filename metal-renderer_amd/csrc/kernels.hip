@@ -870,7 +870,9 @@ __device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o, bool
 // are its primitive's, in its order: v2 - v1, v3 - v1 are the leaf record's
 // e1, e2 bit for bit, as in last_bounce_light_hit) and the occlusion rule
 // (k != target, (t_k, k) < (t_T, target), t_k >= 0), so the query's answer
-// is unchanged.
+// is unchanged — bit for bit in the precise build; in the fast build the
+// compiler may contract this inlined tri_bary differently from the leaf
+// loop's (as origin_occludes), so a near-tie can flip within the 1e-2 gate.
 template <int MODE>
 __device__ __forceinline__ bool lights_occlude(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
                                                float tT) {
