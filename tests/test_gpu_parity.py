@@ -155,6 +155,78 @@ def test_render_parity_precise(gpu, mrt_mod, oracle_mod, scene, W, H, L, frames)
     assert st["paths"] == W * H * frames
 
 
+@pytest.mark.parametrize("W,H,L,frames", [(2, 2, 4, 3), (7, 3, 8, 2), (2, 130, 4, 2), (130, 2, 4, 2),
+                                          (65, 65, 1, 2), (63, 129, 8, 1)])
+def test_render_parity_tiny_and_ragged(gpu, mrt_mod, oracle_mod, W, H, L, frames):
+    """Edge shapes: the smallest image (2x2: rayGenerator divides by W - 1 and
+    H - 1, Shaders.metal:75-103, so 1-pixel sizes are rejected with
+    MRT_ERR_INVALID, test_host), two-pixel rows / columns, sizes one off a
+    64x64 tile and an 8x8 candidate-list block (partial tiles, partial
+    waves, the last tile of a row and of the image): the precise build meets
+    test_render_parity_precise's gates against the oracle (the bit-identical
+    share is printed), every pixel is rendered exactly once per frame, and
+    the image's alpha is 1 everywhere."""
+    sc, osc = _scene(mrt_mod, "cornellbox"), _oscene(oracle_mod, mrt_mod, "cornellbox")
+    ref, A_ref = osc.render(W, H, L, SEED, frames, threads=8)
+    img, st = _render_gpu(mrt_mod, sc, W, H, L, frames, precise=True)
+    assert img.shape[:2] == (H, W)
+    rel, rmse, same = pixel_metrics(img, ref)
+    print(f"{W}x{H} L={L} f={frames}: bit-identical {same:.5f}, A gpu {st['active_ray_bounces']} oracle {A_ref}")
+    assert np.mean(rel <= 1e-4) >= 0.999 and rmse <= 1e-3   # the gates of test_render_parity_precise
+    assert abs(st["active_ray_bounces"] - A_ref) <= max(2, A_ref // 1000)
+    assert st["paths"] == W * H * frames
+    assert np.all(img[..., 3] == 1.0)
+
+
+@pytest.mark.parametrize("W,H,shards", [(2, 2, 8), (70, 10, 4), (64, 64, 3)])
+def test_shards_with_no_tile(gpu, mrt_mod, W, H, shards):
+    """Tile shares of an image with fewer 64x64 tiles than ranks: a rank that
+    owns no tile draws (no-op kernels, no error) and renders no path; the
+    shares still sum to the 1-GPU image bitwise."""
+    sc = _scene(mrt_mod, "cornellbox")
+    full, _ = _render_gpu(mrt_mod, sc, W, H, 4, 2, precise=True)
+    acc = np.zeros_like(full)
+    paths, empty = 0, 0
+    for k in range(shards):
+        part, st = _render_gpu(mrt_mod, sc, W, H, 4, 2, precise=True, shard=(k, shards))
+        acc += part
+        paths += st["paths"]
+        empty += st["paths"] == 0
+    assert paths == W * H * 2
+    tiles = ((W + 63) // 64) * ((H + 63) // 64)   # round-robin: ranks >= tiles own none
+    assert empty == max(0, shards - tiles)
+    assert np.array_equal(acc[..., :3], full[..., :3])
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 64), (64, 1), (0, 8)])
+def test_one_pixel_sizes_rejected(gpu, mrt_mod, W, H):
+    """rayGenerator divides by (W - 1) and (H - 1) (Shaders.metal:75-103): a
+    renderer (and a resize) below 2x2 is refused with an error, not rendered
+    as NaN directions."""
+    sc = _scene(mrt_mod, "cornellbox")
+    with pytest.raises(mrt_mod.MrtError):
+        mrt_mod.Renderer(sc, W, H, 4)
+    r = mrt_mod.Renderer(sc, 8, 8, 4)
+    with pytest.raises(mrt_mod.MrtError):
+        r.resize(W, H)
+    r.draw(1)   # still usable at its old size
+    r.close()
+
+
+def test_zero_frame_draw_is_a_noop(gpu, mrt_mod):
+    """draw(0) enqueues nothing: the image, frame index and statistics are
+    unchanged (mrt_renderer_draw_n with n = 0, as a MAX_FRAMES-capped draw)."""
+    sc = _scene(mrt_mod, "cornellbox")
+    r = mrt_mod.Renderer(sc, 48, 32, 4, seed=SEED, precise=True)
+    r.draw(2)
+    a, sa = r.read_image(), r.stats()
+    r.draw(0)
+    b, sb = r.read_image(), r.stats()
+    r.close()
+    assert a.tobytes() == b.tobytes()
+    assert sa["frame_index"] == sb["frame_index"] and sa["paths"] == sb["paths"]
+
+
 @pytest.mark.parametrize("scene,L", [("cornellbox", 4), ("CornellBox-Water-plastic", 8)])
 def test_render_parity_fast(gpu, mrt_mod, oracle_mod, scene, L):
     W, H, frames = 64, 48, 3
