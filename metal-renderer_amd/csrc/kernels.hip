@@ -17,6 +17,9 @@
 #ifndef MRT_PRECISE
 #error "compile with -DMRT_PRECISE=0 or 1"
 #endif
+#ifndef MRT_TU
+#define MRT_TU 0
+#endif
 #if MRT_PRECISE
 #define MRT_NS precise
 #else
@@ -1985,7 +1988,7 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
 // shadow ray's origin (both are p + n * 1e-4, Shaders.metal:171,205), which
 // stays in the lane's ray registers through the shadow query.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPathStateWords = 12;
+[[maybe_unused]] constexpr uint32_t kPathStateWords = 12;
 #ifndef MRT_PATH_WAVES   // 5: 96 VGPRs with 1-3 spilled values (C4 +11 %, C3 +8 % over 4 waves)
 #define MRT_PATH_WAVES 5
 #endif
@@ -2445,6 +2448,7 @@ size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_
   return scene + scratch + (size_t)stack * kBlock * 4;           // stack = LDS entries (|STACK|)
 }
 
+#if MRT_TU != 2   // the per-bounce and path kernels' host side (not in the stream unit)
 // kTopLds: stage only as many top BVH nodes as keep the block's LDS within
 // 1/MRT_BOUNCE_WAVES of the CU less a 2-KB margin for allocation granularity
 // (the VGPR budget allows MRT_BOUNCE_WAVES resident blocks of 4 waves); the
@@ -2604,6 +2608,8 @@ hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_e
   return dispatch_mode<32>(sc, a, grid, grid_out, s);
 }
 
+#endif  // MRT_TU != 2
+
 // wave-local streaming wavefront: whole-scene-in-LDS scenes, the stack in LDS
 template <int STACK>
 hipError_t launch_stream_t(const DeviceScene& sc, const BounceArgs& a, uint32_t grid, hipStream_t s) {
@@ -2634,6 +2640,12 @@ bool stream_ok(const DeviceScene& sc, uint32_t stack_entries) {
 
 }  // namespace
 
+// Translation units (Makefile): MRT_TU 0 = every entry point (precise and
+// diagnostic builds); the fast build is split in two — MRT_TU 1 everything
+// but the stream kernel, MRT_TU 2 the stream kernel alone, compiled with the
+// max-ILP machine scheduler (-amdgpu-sched-strategy=max-ilp: C2 +0.45 %,
+// alternating in one call, while the path kernel loses 0.5 % under it).
+#if MRT_TU != 2
 hipError_t launch_raygen(uint32_t W, uint32_t H, const float* noise, RefRay* rays, hipStream_t s) {
   raygen_kernel<<<dim3(blocks_for(W * H)), dim3(kBlock), 0, s>>>(W, H,
                      reinterpret_cast<const float4*>(noise), rays);
@@ -2841,6 +2853,8 @@ hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* gr
 
 bool path_preferred(const DeviceScene& sc) { return choose_mode(sc) != kAllLds; }
 
+#endif  // MRT_TU != 2
+#if MRT_TU != 1
 bool stream_supported(const DeviceScene& sc, uint32_t stack_entries) { return stream_ok(sc, stack_entries); }
 
 hipError_t stream_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid) {
@@ -2861,6 +2875,7 @@ hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t st
   if (stack_entries <= 24) return launch_stream_t<24>(sc, a, grid, s);
   return launch_stream_t<32>(sc, a, grid, s);
 }
+#endif  // MRT_TU != 1
 
 }  // namespace MRT_NS
 }  // namespace mrt
