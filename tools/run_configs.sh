@@ -9,7 +9,7 @@
 OUT=${1:-gpurun_out/configs}
 mkdir -p $OUT
 run() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 $secs python3 bench.py "$@" > $OUT/cfg_$name.json 2> $OUT/cfg_$name.log; local rc=$?; tail -c 300 $OUT/cfg_$name.json; echo; echo "== $name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-run c1 300 --config c1 --steps 5 --warmup 1
+run c1 300 --config c1 --steps 50 --warmup 5
 run c2 400 --config c2 --steps 100 --warmup 5
 run c2l5 400 --config c2l5 --steps 100 --warmup 5
 run c2s8 200 --config c2 --steps 400 --warmup 10 --shard-of 8 --no-cpu-baseline --pmc profiles/pmc_c2s8.json
