@@ -577,6 +577,9 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 // 2497 Mpaths/s (+28 %), C3 +7.5 %, C3g +5 %, C5 1/8 share +28 % (8 / 16 /
 // 24 / 32 / 48: C4 2456 / 2488 / 2397 / 2281 / 1904).  Shallow all-in-LDS
 // trees lose by it (C2, the stream kernel: slack 2 -1.3 %, 8 -3.4 %).
+#ifndef MRT_CULL_SLACK   // interior_step: cull children only beyond h.t * (1 + 2^-11)
+#define MRT_CULL_SLACK 1
+#endif
 #ifndef MRT_TRAV_SLACK   // traverse(): stream / bounce / stage kernels
 #define MRT_TRAV_SLACK 0
 #endif
@@ -614,6 +617,19 @@ __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
 
 // One interior node: returns the next node to visit (nearest hit child, or a
 // popped entry, or kDone); the other hit children are pushed far-to-near.
+// Culling slack: a child is culled only when its entry lies beyond the
+// current h.t by more than 2^-11 of it.  Box padding (bvh.cpp) is relative to
+// the box's own coordinates, but the ray-triangle test's t error is relative
+// to the ray's distance and grows for tiny or slanted triangles: on the
+// 1M-triangle mesh (1e-3-sized triangles near x, z = 0) a test returned t
+// 1.5e-5 before the padded box's entry, so whether that triangle was found
+// depended on whether a farther hit had shortened h.t first — i.e. on the
+// lane's visiting order, which the slack rounds make timing-dependent (C5:
+// one pixel in 8.3 M differed between identical runs).  Visiting
+// the few boxes just behind h.t makes the answer the brute-force one again in
+// such cases (it never changes an answer: the leaf tests' t <= h.t rule
+// decides).
+[[maybe_unused]] constexpr float kCullScale = 1.0f + 0x1p-11f;
 template <int STACK, int MODE, bool ANY>
 __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const LdsCtx& cx, int32_t node, V3 o,
                                                  const RayBox& rb, float tmin, float tmax, int& sp) {
@@ -623,6 +639,9 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     {
       float4 q[7];
       fetch_node4<MODE>(sc, cx, node, rb, q);
+#if MRT_CULL_SLACK
+      tmax *= kCullScale;   // +inf stays +inf
+#endif
       box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0),
            !(MRT_EMPTY_BOX && MRT_ROWSEL && MODE == kTopLds)>(q, o, rb, tmin, tmax, t);
       r[0] = (int32_t)fbits(q[6].x); r[1] = (int32_t)fbits(q[6].y); r[2] = (int32_t)fbits(q[6].z); r[3] = (int32_t)fbits(q[6].w);
@@ -1933,15 +1952,28 @@ __device__ __forceinline__ bool trav_done(const Trav& tr) { return tr.node == kD
 template <int STACK, int MODE>
 __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, const RayBox& rb,
                                            Hit& h, bool any, uint32_t target, bool& occluded, Trav& tr,
-                                           uint32_t* uv = nullptr) {
+                                           uint32_t* uv = nullptr, bool trl = false) {
+  (void)trl;
+#if MRT_TRACE_PX
+  if (trl) printf("TR round node=%d leaf=%d sp=%d ht=%08x\n", tr.node, tr.leaf, tr.sp, fbits(h.t));
+#endif
   while (tr.node != kDone && tr.node >= 0) {
     LS_ADD(2, 1);
     LS_ADD(3, (uint32_t)__popcll(__ballot(!any)));
     LS_ADD(9, (uint32_t)__popcll(__ballot(any)));
+#if MRT_TRACE_PX
+    const int32_t n0_ = tr.node;
+#endif
     tr.node = interior_step<STACK, MODE, false>(sc, cx, tr.node, o, rb, 0.0f, h.t, tr.sp);
+#if MRT_TRACE_PX
+    if (trl) printf("TR   int %d -> %d sp=%d leaf=%d\n", n0_, tr.node, tr.sp, tr.leaf);
+#endif
     if (tr.node < 0 && tr.leaf == 0) {
       tr.leaf = tr.node;
       tr.node = stack_pop<STACK>(cx, tr.sp);
+#if MRT_TRACE_PX
+      if (trl) printf("TR   park %d pop %d sp=%d\n", tr.leaf, tr.node, tr.sp);
+#endif
     }
     if ((uint32_t)__popcll(__ballot(tr.leaf == 0)) <= (uint32_t)MRT_PATH_SLACK) break;
   }
@@ -1957,10 +1989,16 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
       tr.leaf = 0;
       break;
     }
+#if MRT_TRACE_PX
+    if (trl) printf("TR   leaf %d first=%u cnt=%u -> ht=%08x prim=%u\n", tr.leaf, first, cnt, fbits(h.t), h.prim);
+#endif
     tr.leaf = 0;
     if (tr.node < 0) {
       tr.leaf = tr.node;
       tr.node = stack_pop<STACK>(cx, tr.sp);
+#if MRT_TRACE_PX
+      if (trl) printf("TR   next leaf %d pop %d sp=%d\n", tr.leaf, tr.node, tr.sp);
+#endif
     }
 #if MRT_LEAF_SLACK > 0
     if ((uint32_t)__popcll(__ballot(tr.leaf < 0)) <= (uint32_t)MRT_LEAF_SLACK) break;
@@ -2035,6 +2073,25 @@ __device__ __forceinline__ void begin_nearest(const DeviceScene& sc, const LdsCt
   trav_begin(sc.root, tr);
   h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
 }
+
+// Diagnostic path trace (MRT_TRACE_PX builds only, never the product): the
+// queries of one pixel-frame (MRT_TRACE_X, MRT_TRACE_Y, absolute frame
+// MRT_TRACE_F) printed with their float bits.
+#ifndef MRT_TRACE_PX
+#define MRT_TRACE_PX 0
+#endif
+#if MRT_TRACE_PX
+__device__ __forceinline__ bool trace_lane(const BounceArgs& a, uint32_t tagv) {
+  const uint32_t gslot = tagv & 0x7FFFFFFFu;
+  const uint32_t fj = a.batch == 1u ? 0u : mdiv(gslot, a.div_slots, a.num_slots);
+  uint32_t x, y;
+  slot_pixel_a(gslot - fj * a.num_slots, a, x, y);
+  return x == MRT_TRACE_X && y == MRT_TRACE_Y && a.frame_index + fj == MRT_TRACE_F;
+}
+#define MRT_TRACE(tagv, ...) do { if (trace_lane(a, (tagv))) printf(__VA_ARGS__); } while (0)
+#else
+#define MRT_TRACE(tagv, ...) do {} while (0)
+#endif
 
 template <int STACK, int MODE>
 __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScene sc, BounceArgs a) {
@@ -2143,6 +2200,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       // rounds (whose shading cost is the same however few lanes they shade)
       // are spent on finished nearest queries only
       if (fin && phase == 2) {
+        MRT_TRACE(ps[11 * kBlock], "TR O inline b=%u occluded=%d\n", bounce, (int)occluded);
         if (!occluded) {
           ps[3 * kBlock] = fbits(bitsf(ps[3 * kBlock]) + h.u);
           ps[4 * kBlock] = fbits(bitsf(ps[4 * kBlock]) + h.v);
@@ -2168,7 +2226,12 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       LS_ADD(23, (uint32_t)__popcll(going));
       if (phase != 0 && !fin) {
         const RayBox rb = make_raybox(ro, rd);
-        trav_round<STACK, MODE>(sc, cx, ro, rd, rb, h, phase >= 2, target, occluded, tr);
+#if MRT_TRACE_PX
+        const bool trl = phase == 1 && bounce == MRT_TRACE_B && trace_lane(a, ps[11 * kBlock]);
+#else
+        const bool trl = false;
+#endif
+        trav_round<STACK, MODE>(sc, cx, ro, rd, rb, h, phase >= 2, target, occluded, tr, nullptr, trl);
         fin = trav_done(tr);
       }
     }
@@ -2180,6 +2243,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
     //      Shaders.metal:214-231), then the path's next bounce
     bool next_query = false;
     if (fin && phase == 2) {
+      MRT_TRACE(ps[11 * kBlock], "TR O service b=%u occluded=%d\n", bounce, (int)occluded);
       if (!occluded) {
         ps[3 * kBlock] = fbits(bitsf(ps[3 * kBlock]) + h.u);
         ps[4 * kBlock] = fbits(bitsf(ps[4 * kBlock]) + h.v);
@@ -2201,6 +2265,9 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       const uint32_t gslot = tagv & 0x7FFFFFFFu;
       const bool last = bounce + 1 == L;
       const bool hit_ok = h.found && !(h.t < kDistanceEpsilon);   // :122-126
+      MRT_TRACE(tagv, "TR N b=%u found=%d t=%08x prim=%u u=%08x v=%08x o=%08x %08x %08x d=%08x %08x %08x\n", bounce,
+                (int)h.found, fbits(h.t), h.prim, fbits(h.u), fbits(h.v), fbits(ro.x), fbits(ro.y), fbits(ro.z),
+                fbits(rd.x), fbits(rd.y), fbits(rd.z));
       ShadowRay sh;
       sh.valid = false;
       LS_ADD(13, (uint32_t)__popcll(__ballot(hit_ok)));
@@ -2218,6 +2285,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         // +1.2 %, 1960 -> 1984 Mpaths/s, A/B twice in one call)
         typedef float v4f __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(v4f{s.R.x, s.R.y, s.R.z, 0.0f}, reinterpret_cast<v4f*>(a.radiance + gslot));
+        MRT_TRACE(tagv, "TR E b=%u R=%08x %08x %08x\n", bounce, fbits(s.R.x), fbits(s.R.y), fbits(s.R.z));
         phase = 0;
       } else {
         ps[0 * kBlock] = fbits(s.T.x); ps[1 * kBlock] = fbits(s.T.y); ps[2 * kBlock] = fbits(s.T.z);
@@ -2239,6 +2307,8 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
               !(sc.occ_lights && sroot == sc.occ_root && lights_occlude<MODE>(sc, cx, ro, sh.d, sh.target, tT))) {
             shadow = true;
             phase = 2;
+            MRT_TRACE(tagv, "TR S b=%u target=%u tT=%08x root=%d L=%08x %08x %08x\n", bounce, sh.target, fbits(tT),
+                      sroot, fbits(sh.L.x), fbits(sh.L.y), fbits(sh.L.z));
             rd = sh.d;   // ro = s.o = sh.o
             trav_begin(sroot, tr);
             h.t = tT;

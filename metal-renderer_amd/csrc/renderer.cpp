@@ -1046,6 +1046,21 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
   const mrt::HostScene& h = scene->host;
   const uint32_t T = (uint32_t)h.references.size();
   std::vector<uint8_t> all(T, 1);
+  if (const char* dn = std::getenv("MRT_DUMP_NODE")) {   // diagnostic: one node's rows and its leaf triangles
+    const uint32_t k = (uint32_t)std::strtoul(dn, nullptr, 0);
+    if (k < b.num_nodes) {
+      const float* n = &b.nodes[32 * (size_t)k];
+      for (int i = 0; i < 32; ++i) std::fprintf(stderr, "NODE %u %d %08x %.9g\n", k, i, fbits(n[i]), n[i]);
+      for (int c = 0; c < 4; ++c) {
+        const int32_t r = (int32_t)fbits(n[24 + c]);
+        if (r >= 0 || r == mrt::kEmptyChild) continue;
+        const uint32_t lr = ~(uint32_t)r, first = lr >> mrt::kLeafCountBits, cnt = (lr & (mrt::kMaxLeafSize - 1)) + 1;
+        for (uint32_t t = first; t < first + cnt; ++t)
+          for (int i = 0; i < 12; ++i)
+            std::fprintf(stderr, "TRI %d %u %d %08x\n", c, t, i, fbits(b.tris[12 * (size_t)t + i]));
+      }
+    }
+  }
   int rc = check_tree(
       h, b.root, 0, b.num_nodes, 0, T, b.max_stack, all, [&](uint32_t r) { return &b.nodes[32 * (size_t)r]; },
       [&](uint32_t k) { return &b.tris[12 * (size_t)k]; }, "main tree");
