@@ -496,9 +496,12 @@ static Intersection intersect_bvh(const Scene& sc, const float* o3, float tmin, 
   bool found = false;
   float bt = tmax, bu = 0, bv = 0;
   uint32_t bk = 0;
+  // boxes are culled only beyond bt * (1 + 2^-11): the triangle test's t can
+  // fall before its own padded box's entry for tiny triangles (the kernels'
+  // kCullScale), and the answer must not depend on the order
   auto box = [&](uint32_t n, float& tn) {
     const CpuBvhNode& b = sc.bvh[n];
-    float t0 = tmin, t1 = bt;
+    float t0 = tmin, t1 = bt * (1.0f + 0x1p-11f);
     for (int a = 0; a < 3; ++a) {
       const float x0 = (b.lo[a] - oo[a]) * inv[a], x1 = (b.hi[a] - oo[a]) * inv[a];
       t0 = std::fmax(t0, std::fmin(x0, x1));
