@@ -536,13 +536,18 @@ def main():
         # a longer window of the same steps (~seconds, visible to an outside
         # utilisation sampler); the headline value stays the K timed steps
         n_s, t_s = 0, time.perf_counter()
+        t_report = t_s
         while True:
             step()
             n_s += 1
             if n_s % 10 == 0:
                 r.sync()
-                if time.perf_counter() - t_s >= args.sustain:
+                now = time.perf_counter()
+                if now - t_s >= args.sustain:
                     break
+                if now - t_report >= 30.0:   # progress for long windows (stderr)
+                    t_report = now
+                    print(f"sustain: {n_s} steps in {now - t_s:.1f} s", file=sys.stderr, flush=True)
         r.sync()
         dt_s = time.perf_counter() - t_s
         sustained = {"steps": n_s, "seconds": round(dt_s, 3),
