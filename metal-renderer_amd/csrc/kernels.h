@@ -41,7 +41,11 @@ constexpr uint32_t kMaxBatch = 64;
 // ranges.  A block's output segment holds chunk + kSegSlack rays, where
 // kSegSlack >= (waves per block + 1) * kGrab keeps at least one block able to
 // grab until the input is exhausted (see bounce_kernel).
-constexpr uint32_t kGrab = 128;
+#ifndef MRT_GRAB   // r5, alternating in one call: 64 / 192 lose 1.1-2.6 % / 1.0 % on C2, 2.1 / 0.5 % on C4
+#define MRT_GRAB 128
+#endif
+constexpr uint32_t kGrab = MRT_GRAB;
+static_assert(kGrab % 64 == 0 && (4 + 1) * kGrab <= 1024, "kGrab: whole waves, within kSegSlack");
 constexpr uint32_t kGrabRanges = 16;   // <= 31: the probe's open mask is one 32-bit ballot word
 static_assert(kGrabRanges <= 31, "kGrabRanges");
 #ifndef MRT_GRAB_STRIDE
