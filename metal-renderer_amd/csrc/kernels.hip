@@ -1825,7 +1825,18 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
 // No wave ever waits for another, so any grid and any residency is safe.
 // ---------------------------------------------------------------------------
 template <int STACK, int MODE>
-__global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void stream_kernel(DeviceScene sc, BounceArgs a) {
+// Waves per SIMD the stream kernel's registers allow: 6 (80 VGPRs, 9 values
+// spilled to scratch) under the max-ILP scheduler of its unit (Makefile):
+// C2 +1.7…+3.4 %, L = 5 +4…6 % over 5 waves (96 VGPRs, no spill); 7 / 8
+// waves (23 / 37 spills) lose 6 / 27 %, and 6 waves under the default
+// scheduler only tie (r5, alternating in one call)
+#ifndef MRT_STREAM_WAVES
+#define MRT_STREAM_WAVES 6
+#endif
+#ifndef MRT_STREAM_SPARE   // block slots per CU the stream kernel's persistent grid leaves free (stream_grid_t)
+#define MRT_STREAM_SPARE 1
+#endif
+__global__ __launch_bounds__(kBlock, MRT_STREAM_WAVES) void stream_kernel(DeviceScene sc, BounceArgs a) {
   __shared__ uint32_t s_cnt[kBlock / 64][kStreamMaxL];    // rays queued per level (wave-private rows)
   __shared__ uint32_t s_alive[kBlock / 64][kStreamMaxL];  // survivors per bounce (stats)
   __shared__ uint32_t s_closed;
@@ -2700,7 +2711,13 @@ hipError_t stream_grid_t(const DeviceScene& sc, uint32_t* grid) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, stream_kernel<STACK, kAllLds>, kBlock,
                                                    bounce_lds_bytes(sc, kAllLds, STACK, 0)) != hipSuccess || occ < 1)
     occ = 1;
-  *grid = (uint32_t)prop.multiProcessorCount * (uint32_t)std::min(occ, 8);
+  // one block slot per CU is left to the other render stream's launch and
+  // the accumulate kernel (MRT_STREAM_SPARE): with 6-wave registers the
+  // kernel fits 6 blocks per CU, and 5 of them persistent measured best —
+  // C2 11937 vs 11740 Mpaths/s with all 6 (1344 / 1408 blocks: within
+  // ±0.3 %), per-frame draws 9585 vs 8856 (r5, alternating in one call)
+  const int spare = occ > 1 ? MRT_STREAM_SPARE : 0;
+  *grid = (uint32_t)prop.multiProcessorCount * (uint32_t)std::min(occ - spare, 8);
   return hipSuccess;
 }
 
