@@ -39,7 +39,8 @@ constexpr int kBlock = 256;   // 4 waves of 64 lanes
 #else
 #define MRT_SHADE_BARRIER() do {} while (0)
 #endif
-// Minimum waves per SIMD for the bounce kernel (launch bounds): 5 caps it at
+// Minimum waves per SIMD for the bounce kernel (launch bounds; the stream
+// kernel has its own, MRT_STREAM_WAVES): 5 caps it at
 // 96 VGPRs with 48 B/lane of scratch spills; 6 (80 VGPRs) spills ~140 B/lane
 // and 4 (no spills) hides less latency — 5 measured best with one stream.
 #ifndef MRT_BOUNCE_WAVES
@@ -2354,7 +2355,8 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
 // accumulated strictly in order (the running mean is order-dependent): one
 // thread applies the batch's frames to its pixel in frame order.
 // At most 32 VGPRs (four frames' loads in flight instead of eight): the
-// render kernels hold 5 waves x 96 of a SIMD's 512 VGPRs, so a 32-VGPR
+// render kernels hold 5 waves x 96 of a SIMD's 512 VGPRs (the path kernel;
+// the stream kernel since r5 5 persistent blocks x 80), so a 32-VGPR
 // accumulate wave fits beside them and batch b's accumulate (main stream)
 // runs while batch b + 1 renders on the other stream instead of waiting for
 // its drain (the 2-stream period was launch + ~0.33 ms on C2).  One call,
