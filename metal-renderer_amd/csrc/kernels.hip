@@ -20,6 +20,15 @@
 #ifndef MRT_TU
 #define MRT_TU 0
 #endif
+// The stream kernel's entry points: in unit 2 of the split fast build, or in
+// the whole-file build (0) — and in unit 1 for lane-statistics builds, whose
+// counters (g_lanes) must live in the unit that reads them (unit 2 then
+// emits nothing)
+#ifndef MRT_LANESTATS
+#define MRT_LANESTATS 0
+#endif
+#define MRT_EMIT_STREAM (MRT_TU == 0 || (MRT_TU == 2 && !MRT_LANESTATS) || (MRT_TU == 1 && MRT_LANESTATS))
+#define MRT_EMIT_MAIN (MRT_TU != 2)
 #if MRT_PRECISE
 #define MRT_NS precise
 #else
@@ -2531,7 +2540,7 @@ size_t bounce_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack, uint32_
   return scene + scratch + (size_t)stack * kBlock * 4;           // stack = LDS entries (|STACK|)
 }
 
-#if MRT_TU != 2   // the per-bounce and path kernels' host side (not in the stream unit)
+#if MRT_EMIT_MAIN   // the per-bounce and path kernels' host side (not in the stream unit)
 // kTopLds: stage only as many top BVH nodes as keep the block's LDS within
 // 1/MRT_BOUNCE_WAVES of the CU less a 2-KB margin for allocation granularity
 // (the VGPR budget allows MRT_BOUNCE_WAVES resident blocks of 4 waves); the
@@ -2691,7 +2700,7 @@ hipError_t dispatch(const DeviceScene& sc, const BounceArgs* a, uint32_t stack_e
   return dispatch_mode<32>(sc, a, grid, grid_out, s);
 }
 
-#endif  // MRT_TU != 2
+#endif  // MRT_EMIT_MAIN
 
 // wave-local streaming wavefront: whole-scene-in-LDS scenes, the stack in LDS
 template <int STACK>
@@ -2734,7 +2743,7 @@ bool stream_ok(const DeviceScene& sc, uint32_t stack_entries) {
 // but the stream kernel, MRT_TU 2 the stream kernel alone, compiled with the
 // max-ILP machine scheduler (-amdgpu-sched-strategy=max-ilp: C2 +0.45 %,
 // alternating in one call, while the path kernel loses 0.5 % under it).
-#if MRT_TU != 2
+#if MRT_EMIT_MAIN
 hipError_t launch_raygen(uint32_t W, uint32_t H, const float* noise, RefRay* rays, hipStream_t s) {
   raygen_kernel<<<dim3(blocks_for(W * H)), dim3(kBlock), 0, s>>>(W, H,
                      reinterpret_cast<const float4*>(noise), rays);
@@ -2942,8 +2951,8 @@ hipError_t path_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* gr
 
 bool path_preferred(const DeviceScene& sc) { return choose_mode(sc) != kAllLds; }
 
-#endif  // MRT_TU != 2
-#if MRT_TU != 1
+#endif  // MRT_EMIT_MAIN
+#if MRT_EMIT_STREAM
 bool stream_supported(const DeviceScene& sc, uint32_t stack_entries) { return stream_ok(sc, stack_entries); }
 
 hipError_t stream_grid(const DeviceScene& sc, uint32_t stack_entries, uint32_t* grid) {
@@ -2964,7 +2973,7 @@ hipError_t launch_stream(const DeviceScene& sc, const BounceArgs& a, uint32_t st
   if (stack_entries <= 24) return launch_stream_t<24>(sc, a, grid, s);
   return launch_stream_t<32>(sc, a, grid, s);
 }
-#endif  // MRT_TU != 1
+#endif  // MRT_EMIT_STREAM
 
 }  // namespace MRT_NS
 }  // namespace mrt
