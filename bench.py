@@ -107,6 +107,9 @@ def parse():
                    help="N > 1: exchange inside each step instead of overlapping it with the next step's draw")
     p.add_argument("--check-image", action="store_true",
                    help="N>1: rank 0 renders the frame alone afterwards and asserts the exchanged image is bitwise equal")
+    p.add_argument("--check-image-tolerance", action="store_true",
+                   help="with --check-image: accept <= 1e-5 of the pixels differing, each within rel-L2 1e-3 "
+                        "(the differing count is reported either way)")
     p.add_argument("--exchange-backend", default="rccl", choices=["rccl", "host"],
                    help="rccl: libmrt's RCCL collective (one process per GPU); host: packed tiles through host "
                         "memory and a gloo gather (rehearsal of the N>1 path with several ranks on one GPU)")
@@ -246,7 +249,9 @@ def cpu_baseline(cfg, frames):
     """The CPU oracle (scalar C++ restatement of the path, oracle/) timed on
     this host on a bounded sample of the same workload, its
     nearest hits through a binned-SAH BVH (oracle ORC_BVH: the same answers
-    as its brute force, tests/test_oracle.py) — "same BVH", not brute force.
+    as its brute force, tests/test_oracle.py; its culling slack, 2^-6 of the
+    hit's t, is independent of the kernels' 2^-11) — "same
+    BVH", not brute force.
     C2 runs in full (all `frames` = spp frames of the whole image) on every
     CPU of the process's share, and 2 frames on one thread give the scalar
     rate.  Other scenes run one frame of a row band sized from a pilot band to
@@ -731,23 +736,22 @@ def main():
             r1.draw(spp)
             ref = r1.read_image()
             r1.close()
-            same = got[..., :3].tobytes() == ref[..., :3].tobytes()
-            result["image_check"] = "bitwise equal to the 1-GPU render" if same else "MISMATCH"
-            if not same and not args.precise and st["kernel"] == 1:
-                # the fast build's path kernel: the order of a wave's traversal
-                # rounds depends on timing, and at a near-tie pixel a contracted
-                # float test can accept a triangle whose box another order culls
-                # (DESIGN §3.1): a few pixels may differ at rounding level.  The
-                # precise build (--precise) is bitwise; here the gate is
-                # <= 1e-5 of the pixels, each within rel-L2 1e-3
-                import numpy as np
+            import numpy as np
+            n_diff = int((got[..., :3] != ref[..., :3]).any(-1).sum())
+            same = n_diff == 0
+            result["image_check"] = ("bitwise equal to the 1-GPU render" if same else
+                                     f"MISMATCH: {n_diff} of {W * H} pixels differ from the 1-GPU render")
+            result["image_check_pixels_differing"] = n_diff
+            if not same and args.check_image_tolerance:
+                # opt-in gate (--check-image-tolerance): <= 1e-5 of the pixels,
+                # each within rel-L2 1e-3.  The default is bitwise: the near-tie
+                # order dependence of DESIGN §3.1 is fixed by the culling slack
                 g, c = got[..., :3].astype(np.float64), ref[..., :3].astype(np.float64)
                 rel = np.sqrt(((g - c) ** 2).sum(-1)) / (np.sqrt((c ** 2).sum(-1)) + 1e-3)
-                n_diff = int((got[..., :3] != ref[..., :3]).any(-1).sum())
                 same = n_diff <= 1e-5 * W * H and float(rel.max()) <= 1e-3
                 result["image_check"] = (f"{n_diff} of {W * H} pixels differ from the 1-GPU render, max rel-L2 "
-                                         f"{float(rel.max()):.2e} (fast path kernel; the precise build is bitwise)"
-                                         if same else "MISMATCH")
+                                         f"{float(rel.max()):.2e} (within the --check-image-tolerance gate)"
+                                         if same else result["image_check"])
             if not same:   # which tiles (and whose) differ
                 import numpy as np
                 diff = (got[..., :3] != ref[..., :3]).any(-1)

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 8
+#define MRT_ABI_VERSION 9
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -403,6 +403,24 @@ int mrt_debug_lanes(uint64_t* out, size_t n, int reset);
  * shard_count nranks) unpacks slabs 1..N-1 into its image with the RCCL
  * path's own unpack.  Synchronises the renderer. */
 int mrt_debug_exchange_unpack(mrt_renderer* r, uint32_t nranks, const float* gathered, size_t floats);
+/* Test entry (ABI 9, host only, no device): the traversal culling slack each
+ * ray's nearest hit needs in the scene's main tree.  For ray record i
+ * (origin, minDistance, direction, maxDistance at `stride` bytes) and its
+ * brute-force nearest hit intersections[i] (reference layout, distance < 0 =
+ * miss): out[4i + 0..1] = the largest (t_entry - t_hit) / t_hit over the child
+ * boxes on the path from the root to the hit primitive's leaf, with the slab
+ * test in the precise build's arithmetic ((p - o) * inv) and the fast build's
+ * (fma(p, inv, -o * inv)); out[4i + 2..3] = the same for the near ties — the
+ * triangles sharing a vertex position with the hit whose triangle test passes
+ * within first-order rounding bounds (4u per operation chain), each at the
+ * smallest t those bounds allow, within 2^-10 of t_hit (what a differently
+ * rounding triangle test may report instead).  +inf if the ray
+ * misses one of those boxes altogether, -inf for none.  The kernels cull a
+ * child only when its entry lies beyond h.t * (1 + 2^-11) (kernels.hip
+ * kCullScale): every value below 2^-11 is a hit no visiting order can lose
+ * (DESIGN.md §3.1). */
+int mrt_debug_box_margin(const mrt_scene* scene, const void* rays, uint32_t stride, uint32_t count,
+                         const void* intersections, float* out);
 /* Number of HIP devices visible (0 when none; never fails). */
 int mrt_device_count(void);
 

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1075,6 +1076,122 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
       h, scene->occ_root, scene->occ_node_base, occ_nodes, T, (uint32_t)scene->occ_keep.size(), scene->occ_max_stack,
       kept, [&](uint32_t r) { return &scene->occ_nodes[32 * (size_t)(r - scene->occ_node_base)]; },
       [&](uint32_t k) { return &scene->occ_tris[12 * (size_t)(k - T)]; }, "occluder tree");
+}
+
+int mrt_debug_box_margin(const mrt_scene* scene, const void* rays, uint32_t stride, uint32_t count,
+                         const void* intersections, float* out) {
+  if (!scene || (count && (!rays || !intersections || !out))) return fail(MRT_ERR_INVALID, "null argument");
+  if (stride < 32 || stride % 4) return fail(MRT_ERR_INVALID, "ray stride must be >= 32 and a multiple of 4");
+  const mrt::BvhResult& b = scene->bvh;
+  const mrt::HostScene& h = scene->host;
+  const uint32_t T = (uint32_t)h.references.size();
+  // (parent node, child slot) of every interior node and of every primitive's leaf
+  struct Up { uint32_t node, slot; };
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  std::vector<Up> node_up(b.num_nodes, Up{kNone, 0}), prim_up(T, Up{kNone, 0});
+  if (b.root >= 0)
+    for (uint32_t n = 0; n < b.num_nodes; ++n)
+      for (uint32_t c = 0; c < 4; ++c) {
+        const int32_t ref = (int32_t)fbits(b.nodes[32 * (size_t)n + 24 + c]);
+        if (ref == mrt::kEmptyChild) continue;
+        if (ref >= 0) { node_up[ref] = Up{n, c}; continue; }
+        const uint32_t lr = ~(uint32_t)ref, first = lr >> mrt::kLeafCountBits, cnt = (lr & (mrt::kMaxLeafSize - 1)) + 1;
+        for (uint32_t k = first; k < first + cnt; ++k) prim_up[fbits(b.tris[12 * (size_t)k + 3])] = Up{n, c};
+      }
+  // triangles around each vertex position (vertex records are per (position,
+  // normal), so corners are matched by their position bits)
+  std::vector<std::pair<uint64_t, uint32_t>> corner;   // (hash of position, triangle)
+  corner.reserve(3 * (size_t)T);
+  auto pos_key = [&](uint32_t vi) {
+    const float* v = h.vertices[vi].v;
+    return ((uint64_t)fbits(v[0]) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)fbits(v[1]) * 0xC2B2AE3D27D4EB4Full) ^
+           ((uint64_t)fbits(v[2]) * 0x165667B19E3779F9ull);
+  };
+  for (uint32_t t = 0; t < T; ++t)
+    for (int c = 0; c < 3; ++c) corner.emplace_back(pos_key(h.references[t].tri[c]), t);
+  std::sort(corner.begin(), corner.end());
+  const uint8_t* rp = static_cast<const uint8_t*>(rays);
+  const mrt::RefIntersection* is = static_cast<const mrt::RefIntersection*>(intersections);
+  for (uint32_t i = 0; i < count; ++i) {
+    const float* f = reinterpret_cast<const float*>(rp + (size_t)i * stride);
+    float* o4 = out + 4 * (size_t)i;
+    o4[0] = o4[1] = o4[2] = o4[3] = -INFINITY;   // a miss, or a leaf-root tree (no box above the triangle)
+    if (!(is[i].distance >= 0.0f) || is[i].triangleIndex >= T || prim_up[is[i].triangleIndex].node == kNone) continue;
+    const float tmin = f[3];
+    float inv[3], oinv[3];
+    for (int a = 0; a < 3; ++a) {   // kernels.hip make_raybox (the fast build's reciprocal correctly rounded here)
+      const float d = f[4 + a], dd = std::fabs(d) > 1e-20f ? d : std::copysign(1e-20f, d);
+      inv[a] = 1.0f / dd;
+      oinv[a] = f[a] * inv[a];
+    }
+    // the worst (t_entry - t) / t over the boxes above primitive k's leaf
+    auto margin = [&](uint32_t k, float t, float* worst) {
+      for (Up u = prim_up[k]; u.node != kNone; u = node_up[u.node]) {
+        const float* n = &b.nodes[32 * (size_t)u.node];
+        for (int form = 0; form < 2; ++form) {   // 0: precise (p - o) * inv, 1: fast fma(p, inv, -o * inv)
+          float tn = tmin, tf = INFINITY;
+          for (int a = 0; a < 3; ++a) {
+            const float lo = n[8 * a + u.slot], hi = n[8 * a + 4 + u.slot];
+            const float x0 = form ? std::fma(lo, inv[a], -oinv[a]) : (lo - f[a]) * inv[a];
+            const float x1 = form ? std::fma(hi, inv[a], -oinv[a]) : (hi - f[a]) * inv[a];
+            tn = std::fmax(tn, std::fmin(x0, x1));
+            tf = std::fmin(tf, std::fmax(x0, x1));
+          }
+          // a box the ray's slab interval misses altogether: no culling slack finds the triangle
+          worst[form] = std::fmax(worst[form], tn <= tf ? (tn - t) / t : INFINITY);
+        }
+      }
+    };
+    const uint32_t hit = is[i].triangleIndex;
+    const float t_hit = is[i].distance;
+    margin(hit, t_hit, o4);
+    // near ties: triangles sharing a vertex position with the hit whose
+    // Moller-Trumbore test some rounding of its float operations could pass
+    // (a build that rounds differently — FMA contraction, an approximate
+    // reciprocal — may report one of them instead, at its own t: DESIGN.md
+    // §3.1's ray).  b1, b2 and t are evaluated exactly (double, on the float
+    // inputs) with first-order error bounds of 4u per operation chain; a
+    // neighbour counts when every test passes within its bound, and its slack
+    // is taken at the smallest t the bound allows.
+    const double o[3] = {f[0], f[1], f[2]}, d[3] = {f[4], f[5], f[6]};
+    std::vector<uint32_t> ring;
+    for (int c = 0; c < 3; ++c) {
+      const uint64_t key = pos_key(h.references[hit].tri[c]);
+      for (auto it = std::lower_bound(corner.begin(), corner.end(), std::make_pair(key, 0u));
+           it != corner.end() && it->first == key; ++it)
+        if (it->second != hit) ring.push_back(it->second);
+    }
+    std::sort(ring.begin(), ring.end());
+    ring.erase(std::unique(ring.begin(), ring.end()), ring.end());
+    auto norm = [](const double* x) { return std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]); };
+    for (uint32_t k : ring) {
+      const float* v0 = h.vertices[h.references[k].tri[0]].v;
+      const float* v1 = h.vertices[h.references[k].tri[1]].v;
+      const float* v2 = h.vertices[h.references[k].tri[2]].v;
+      double e1[3], e2[3], sv[3];   // e1, e2 as the kernels' float records hold them
+      for (int a = 0; a < 3; ++a) {
+        e1[a] = (double)(v1[a] - v0[a]);
+        e2[a] = (double)(v2[a] - v0[a]);
+        sv[a] = o[a] - (double)v0[a];
+      }
+      const double p[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
+      const double q[3] = {sv[1] * e1[2] - sv[2] * e1[1], sv[2] * e1[0] - sv[0] * e1[2], sv[0] * e1[1] - sv[1] * e1[0]};
+      const double det = e1[0] * p[0] + e1[1] * p[1] + e1[2] * p[2];
+      if (det == 0.0) continue;
+      const double b1 = (sv[0] * p[0] + sv[1] * p[1] + sv[2] * p[2]) / det;
+      const double b2 = (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]) / det;
+      const double t = (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]) / det;
+      constexpr double u4 = 4.0 * 0x1p-24;
+      const double np = norm(p), nq = norm(sv) * norm(e1) + norm(q), ad = std::fabs(det);
+      const double eb1 = u4 * (norm(sv) * np + std::fabs(b1) * norm(e1) * np) / ad;
+      const double eb2 = u4 * (norm(d) * nq + std::fabs(b2) * norm(e1) * np) / ad;
+      const double et = u4 * (norm(e2) * nq + std::fabs(t) * norm(e1) * np) / ad;
+      if (!(b1 >= -eb1 && b2 >= -eb2 && b1 + b2 <= 1.0 + eb1 + eb2 && t + et >= tmin && t - et > 0.0)) continue;
+      if (!(std::fabs(t - t_hit) <= 0x1p-10 * t_hit + et)) continue;
+      margin(k, (float)(t - et), o4 + 2);
+    }
+  }
+  return MRT_OK;
 }
 
 int mrt_scene_destroy(mrt_scene* scene) {

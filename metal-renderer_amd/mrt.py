@@ -151,7 +151,7 @@ EXPORTED = [
     "mrt_renderer_exchange_flush", "mrt_renderer_tiles_read", "mrt_renderer_tiles_write",
     "mrt_image_load_exr", "mrt_renderer_load_reference", "mrt_renderer_display",
     "mrt_renderer_display_enqueue", "mrt_renderer_display_map",
-    "mrt_debug_lanes", "mrt_debug_exchange_unpack",
+    "mrt_debug_lanes", "mrt_debug_exchange_unpack", "mrt_debug_box_margin",
 ]
 
 _lib = None
@@ -206,6 +206,7 @@ def lib() -> ctypes.CDLL:
         "mrt_debug_wave_times": [vp, ctypes.c_size_t],
         "mrt_debug_lanes": [vp, ctypes.c_size_t, c_int],
         "mrt_debug_exchange_unpack": [vp, u32, vp, ctypes.c_size_t],
+        "mrt_debug_box_margin": [vp, vp, u32, u32, vp, vp],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
         "mrt_tiles_packed_floats": [u32, u32, u32, u32, ctypes.POINTER(u64)],
         "mrt_display": [vp, vp, vp, u32, u32, u32, ctypes.c_float, vp],
@@ -294,6 +295,21 @@ class Scene:
 
     def check_bvh(self) -> None:
         _check(lib().mrt_scene_check_bvh(self._h), "mrt_scene_check_bvh")
+
+    def box_margin(self, rays, intersections):
+        """Host-only test entry mrt_debug_box_margin: per ray (numpy records,
+        reference layout) and its nearest hit, the culling slack the hit needs
+        in the main tree, as (precise, fast) slab arithmetic, then the same for
+        the hit's near ties (mrt.h): float32 [n, 4]."""
+        import numpy as np
+        rays = np.ascontiguousarray(rays)
+        intersections = np.ascontiguousarray(intersections)
+        assert len(rays) == len(intersections) and intersections.dtype.itemsize == 16
+        out = np.zeros((len(rays), 4), np.float32)
+        p = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+        _check(lib().mrt_debug_box_margin(self._h, p(rays), rays.dtype.itemsize, len(rays), p(intersections), p(out)),
+               "mrt_debug_box_margin")
+        return out
 
     def close(self):
         if self._h:

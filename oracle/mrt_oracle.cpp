@@ -23,7 +23,7 @@
 //       - SceneKit OBJ import (renderer/Renderer.mm:265-268): own OBJ/MTL
 //         parser, one geometry element per `usemtl`, Ka -> emission.
 //   * Pinned against the reference's only fixtures: the Mitsuba golden EXRs
-//     in renderer/Media/reference (statistical: tests/test_oracle_golden.py)
+//     in renderer/Media/reference (statistical: tests/test_oracle.py:22-48)
 //     plus known-answer values derived from the reference source.
 //   * The clock-seeded noise (renderer/Renderer.mm:109-112,486-490) is replaced
 //     by the deterministic serialized schedule of SURVEY.md Appendix A.3.
@@ -485,7 +485,20 @@ static void build_cpu_bvh(const Scene& sc) {
 
 static inline float safe_inv(float d) { return 1.0f / (std::fabs(d) > 1e-20f ? d : std::copysign(1e-20f, d)); }
 
-static Intersection intersect_bvh(const Scene& sc, const float* o3, float tmin, const float* d3, float tmax) {
+// Culling rule of the CPU BVH's traversal.  It must not share the kernels'
+// error mode (their children are culled beyond h.t * (1 + 2^-11), kernels.hip
+// kCullScale), or a triangle the kernels miss by the same
+// rounding would be missed here too and the comparison would pass:
+//   kCullWide — boxes culled only beyond bt * (1 + 2^-6): strictly more
+//               conservative than the kernels' slack, so a kernel answer equal
+//               to this one shows the kernels' slack sufficed for that ray;
+//   kCullNone — no culling by the current hit at all: every box whose slab
+//               interval meets [tmin, tmax] is visited, which is the brute
+//               force over every triangle whose padded box the ray enters.
+enum CullMode : int { kCullWide = 0, kCullNone = 1 };
+
+static Intersection intersect_bvh(const Scene& sc, const float* o3, float tmin, const float* d3, float tmax,
+                                  int cull = kCullWide) {
   Intersection r{-1.0f, 0xFFFFFFFFu, {0.0f, 0.0f}};
   if (tmax < 0.0f) return r;   // disabled ray (renderer/Shaders.metal:119,124,173)
   std::call_once(sc.bvh_once, build_cpu_bvh, std::cref(sc));
@@ -496,12 +509,10 @@ static Intersection intersect_bvh(const Scene& sc, const float* o3, float tmin, 
   bool found = false;
   float bt = tmax, bu = 0, bv = 0;
   uint32_t bk = 0;
-  // boxes are culled only beyond bt * (1 + 2^-11): the triangle test's t can
-  // fall before its own padded box's entry for tiny triangles (the kernels'
-  // kCullScale), and the answer must not depend on the order
+  const float ray_tmax = tmax;
   auto box = [&](uint32_t n, float& tn) {
     const CpuBvhNode& b = sc.bvh[n];
-    float t0 = tmin, t1 = bt * (1.0f + 0x1p-11f);
+    float t0 = tmin, t1 = cull == kCullNone ? ray_tmax : bt * (1.0f + 0x1p-6f);
     for (int a = 0; a < 3; ++a) {
       const float x0 = (b.lo[a] - oo[a]) * inv[a], x1 = (b.hi[a] - oo[a]) * inv[a];
       t0 = std::fmax(t0, std::fmin(x0, x1));
@@ -1035,6 +1046,27 @@ void orc_intersect_bvh(const orc_scene* sc, const void* rays, uint32_t stride, u
   }
 }
 
+// the same on `threads` threads with an explicit culling rule (0 = kCullWide,
+// 1 = kCullNone; see intersect_bvh)
+void orc_intersect_bvh_mt(const orc_scene* sc, const void* rays, uint32_t stride, uint32_t count, void* isect_out,
+                          uint32_t threads, uint32_t cull) {
+  const uint8_t* p = (const uint8_t*)rays;
+  Intersection* out = (Intersection*)isect_out;
+  std::call_once(sc->s.bvh_once, build_cpu_bvh, std::cref(sc->s));
+  std::atomic<uint32_t> next{0};
+  auto work = [&]() {
+    for (uint32_t i0 = next.fetch_add(1024); i0 < count; i0 = next.fetch_add(1024))
+      for (uint32_t i = i0; i < std::min(count, i0 + 1024u); ++i) {
+        const float* f = (const float*)(p + (size_t)i * stride);
+        out[i] = intersect_bvh(sc->s, f, f[3], f + 4, f[7], cull ? kCullNone : kCullWide);
+      }
+  };
+  if (threads <= 1) { work(); return; }
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < threads; ++t) th.emplace_back(work);
+  for (auto& t : th) t.join();
+}
+
 // ---- whole-frame driver: performRaytracing: (renderer/Renderer.mm:500-585) --
 // Renders frames [frame_begin, frame_end) into image_rgba (W*H*4, row 0 =
 // bottom), accumulating as accumulateImage does.  Rows are handed out one at
@@ -1049,12 +1081,15 @@ void orc_intersect_bvh(const orc_scene* sc, const void* rays, uint32_t stride, u
 //   2 ORC_NO_ACCUMULATE    ACCUMULATE_IMAGE false: the image is the last frame
 //   4 ORC_DEBUG_MATERIAL   DEBUG_MATERIAL 1: radiance := Fresnel at each hit
 //   8 ORC_BVH              nearest hits through the CPU BVH (the cpu_baseline
-//                          leg) instead of brute force — the same answers
+//                          leg) instead of brute force — the same answers;
+//                          boxes culled beyond bt * (1 + 2^-6) (kCullWide)
+//  16 ORC_BVH_NOCULL       with ORC_BVH: no culling by the current hit (kCullNone)
 int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLength, uint64_t seed,
                uint32_t frame_begin, uint32_t frame_end, uint32_t threads, const uint8_t* pixel_mask,
                float* image_rgba, uint64_t* active_out, uint32_t flags) {
   if (W < 2 || H < 2 || maxPathLength == 0) return -1;
   const bool use_bvh = (flags & 8u) != 0;
+  const int cull = (flags & 16u) ? kCullNone : kCullWide;
   const bool use_packets = !use_bvh && sc->s.references.size() >= g_packet_threshold;
   const bool debug_material = (flags & 4u) != 0, accumulate = (flags & 2u) == 0;
   if (use_bvh) std::call_once(sc->s.bvh_once, build_cpu_bvh, std::cref(sc->s));
@@ -1117,10 +1152,12 @@ int orc_render(const orc_scene* sc, uint32_t W, uint32_t H, uint32_t maxPathLeng
           rayGenerator(ray, x, y, W, H, raygenNoise);
           for (uint32_t i = 0; i < maxPathLength; ++i) {
             if (ray.maxDistance >= 0.0f) ++local;
-            const auto isect = use_bvh ? intersect_bvh : intersect_one;
-            Intersection is = isect(sc->s, ray.origin, ray.minDistance, ray.direction, ray.maxDistance);
+            auto isect = [&](const float* o, float t0, const float* d, float t1) {
+              return use_bvh ? intersect_bvh(sc->s, o, t0, d, t1, cull) : intersect_one(sc->s, o, t0, d, t1);
+            };
+            Intersection is = isect(ray.origin, ray.minDistance, ray.direction, ray.maxDistance);
             intersectionHandler(sc->s, is, ray, sray, x, y, f, maxPathLength, iterNoise[i], debug_material);
-            Intersection is2 = isect(sc->s, sray.origin, sray.minDistance, sray.direction, sray.maxDistance);
+            Intersection is2 = isect(sray.origin, sray.minDistance, sray.direction, sray.maxDistance);
             lightSamplingHandler(is2, ray, sray);
           }
           accumulateImage(ray, image_rgba + 4 * pix, f, accumulate);

@@ -59,7 +59,11 @@ _lib = None
 STATIC_NOISE = 1      # ANIMATE_NOISE 0
 NO_ACCUMULATE = 2     # ACCUMULATE_IMAGE false
 DEBUG_MATERIAL = 4    # DEBUG_MATERIAL 1
-BVH = 8               # nearest hits through the CPU BVH (same answers as brute force)
+BVH = 8               # nearest hits through the CPU BVH (same answers as brute force); boxes are
+                      # culled only beyond the current hit's t * (1 + 2^-6), far wider than the
+                      # kernels' 2^-11 slack, so the two do not share an error mode
+BVH_NOCULL = 16       # with BVH: no culling by the current hit at all (every box the ray's
+                      # [tmin, tmax] slab interval enters)
 
 
 def build() -> None:
@@ -88,6 +92,7 @@ def lib() -> ctypes.CDLL:
         L.orc_raygen.argtypes = [u32, u32, vp, vp]
         L.orc_intersect.argtypes = [vp, vp, u32, u32, vp]
         L.orc_intersect_bvh.argtypes = [vp, vp, u32, u32, vp]
+        L.orc_intersect_bvh_mt.argtypes = [vp, vp, u32, u32, vp, u32, u32]
         L.orc_shade.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, u32]
         L.orc_resolve.argtypes = [u32, vp, vp, vp]
         L.orc_accumulate.argtypes = [u32, u32, vp, vp, u32]
@@ -154,11 +159,16 @@ class OracleScene:
         lib().orc_intersect(self.h, _p(rays), rays.dtype.itemsize, len(rays), _p(out))
         return out
 
-    def intersect_bvh(self, rays: np.ndarray) -> np.ndarray:
-        """intersect() through the CPU baseline's BVH (identical answers)."""
+    def intersect_bvh(self, rays: np.ndarray, threads: int = 1, nocull: bool = False) -> np.ndarray:
+        """intersect() through the CPU baseline's BVH (identical answers);
+        nocull: no culling by the current hit (see BVH_NOCULL)."""
         rays = np.ascontiguousarray(rays)
         out = np.zeros(len(rays), ISECT_DTYPE)
-        lib().orc_intersect_bvh(self.h, _p(rays), rays.dtype.itemsize, len(rays), _p(out))
+        if threads == 1 and not nocull:
+            lib().orc_intersect_bvh(self.h, _p(rays), rays.dtype.itemsize, len(rays), _p(out))
+        else:
+            lib().orc_intersect_bvh_mt(self.h, _p(rays), rays.dtype.itemsize, len(rays), _p(out), threads,
+                                       1 if nocull else 0)
         return out
 
     def shade(self, W, H, frame_index, max_path_length, noise, isect, rays, srays, flags=0):
@@ -166,7 +176,7 @@ class OracleScene:
 
     def render(self, W, H, L, seed, frames, frame_begin=0, threads=1, image=None, pixel_mask=None, flags=0):
         """Returns (image[H,W,4] float32, active ray-bounces A); flags: STATIC_NOISE,
-        NO_ACCUMULATE, DEBUG_MATERIAL, BVH."""
+        NO_ACCUMULATE, DEBUG_MATERIAL, BVH, BVH_NOCULL."""
         if image is None:
             image = np.zeros((H, W, 4), np.float32)
         active = np.zeros(1, np.uint64)
