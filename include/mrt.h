@@ -52,7 +52,10 @@ typedef enum mrt_status {
   MRT_ERR_IO = -2,        /* scene / image file error */
   MRT_ERR_HIP = -3,       /* HIP runtime error (no device, launch failure, ...) */
   MRT_ERR_NOMEM = -4,
-  MRT_ERR_STATE = -5      /* call not valid in the handle's current state */
+  MRT_ERR_STATE = -5,     /* call not valid in the handle's current state */
+  MRT_ERR_COMM = -6       /* ABI 9: an RCCL collective reported an asynchronous error or did not complete
+                             within the communicator's timeout; the communicator is aborted and every
+                             later use of it fails with this status (renderers stay usable) */
 } mrt_status;
 
 /* flags */
@@ -360,8 +363,23 @@ int mrt_comm_unique_id(void* id, size_t bytes);   /* ncclGetUniqueId: bytes >= M
 int mrt_comm_create(const void* id, uint32_t nranks, uint32_t rank, int device, mrt_comm** out);
 int mrt_comm_destroy(mrt_comm* comm);
 int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* comm, uint32_t mode);
-/* Complete a deferred (MRT_EXCHANGE_OVERLAP) exchange on the renderer's stream. */
+/* Complete a deferred (MRT_EXCHANGE_OVERLAP) exchange on the renderer's stream
+ * and wait, bounded by the communicator's timeout, for the collective to
+ * complete on the device (ABI 9; mrt_renderer_sync / _read_image wait the same
+ * way).  Meanwhile the communicator's asynchronous error is polled
+ * (ncclCommGetAsyncError); on an error or at the timeout it is aborted
+ * (ncclCommAbort) and MRT_ERR_COMM is returned with mrt_last_error() set. */
 int mrt_renderer_exchange_flush(mrt_renderer* r);
+/* ABI 9: the bound of those waits (0 = the default, 120000 ms), and a
+ * non-blocking health check (MRT_OK, or MRT_ERR_COMM once aborted or when an
+ * asynchronous error is pending — which aborts it). */
+int mrt_comm_set_timeout(mrt_comm* comm, uint32_t timeout_ms);
+int mrt_comm_check(mrt_comm* comm);
+/* Test entry (ABI 9): inject a failure into the communicator's health checks
+ * — 1: an asynchronous error is reported; 2: its collectives never complete
+ * (the bounded wait reaches the timeout); 0: none.  The abort that follows is
+ * the real one (ncclCommAbort). */
+int mrt_debug_comm_fail(mrt_comm* comm, uint32_t mode);
 /* Host-side exchange for hosts with their own transport (MPI, gloo, ...):
  * the renderer's owned tiles packed to host memory (mrt_tiles_packed_floats
  * floats for its shard), and another shard's packed tiles written into the
@@ -421,6 +439,10 @@ int mrt_debug_exchange_unpack(mrt_renderer* r, uint32_t nranks, const float* gat
  * (DESIGN.md §3.1). */
 int mrt_debug_box_margin(const mrt_scene* scene, const void* rays, uint32_t stride, uint32_t count,
                          const void* intersections, float* out);
+/* Test entry (ABI 9, host only): q[i] = n[i] / d through the kernels' exact
+ * division by a launch divisor (kernels.h magic_div: the multiplier the
+ * renderer passes, applied as the kernels' mulhi + shift), n[i] < 2^31. */
+int mrt_debug_magic_div(uint32_t d, const uint32_t* n, uint32_t count, uint32_t* q);
 /* Number of HIP devices visible (0 when none; never fails). */
 int mrt_device_count(void);
 

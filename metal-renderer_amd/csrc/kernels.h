@@ -80,6 +80,20 @@ inline MagicDiv magic_div(uint32_t d) {
   const unsigned long long p = 1ull << (31 + l);
   return {(uint32_t)((p + d - 1) / d), l - 1};
 }
+// The kernels' quotient (kernels.hip mdiv: __umulhi(n, m) >> sh) restated on
+// the host, and the check draw_n runs on every launch's divisors: m = 0 means
+// d = 1, so a multiplier left zero for a divisor d > 1 (or one computed for
+// another d) fails at the floor steps below instead of dividing by 1.
+inline uint32_t mdiv_host(uint32_t n, MagicDiv m) {
+  return m.m ? (uint32_t)(((unsigned long long)n * m.m) >> 32) >> m.sh : n;
+}
+inline bool magic_ok(MagicDiv m, uint32_t d) {
+  if (d == 0) return false;
+  const uint32_t top = 0x7FFFFFFFu, ns[5] = {0u, d - 1u, d < top ? d : top, top - top % d, top};
+  for (uint32_t n : ns)
+    if (mdiv_host(n, m) != n / d) return false;
+  return true;
+}
 
 struct BounceArgs {
   uint32_t width, height;

@@ -90,13 +90,14 @@ NoiseSchedule::Chunk* NoiseSchedule::find(int64_t k) {
   return nullptr;
 }
 
-hipError_t NoiseSchedule::slot_for(int64_t k, uint64_t seq, Chunk** out) {
+hipError_t NoiseSchedule::slot_for(int64_t k, uint64_t seq, Chunk** out, int64_t keep_lo, int64_t keep_hi) {
   (void)k;
   Chunk* best = nullptr;
   for (auto& up : chunks_) {
     Chunk* c = up.get();
     if (!c->uploaded) { best = c; break; }
     if (seq && c->pin == seq) continue;   // read by the draw being enqueued
+    if (c->index >= keep_lo && c->index <= keep_hi) continue;   // about to be read by the caller's draw
     if (c->used && hipEventQuery(c->last_use) != hipSuccess) continue;   // a queued draw still reads it
     if (hipEventQuery(c->ready) != hipSuccess) continue;                 // its upload is still landing
     if (!best || c->lru < best->lru) best = c;
@@ -122,9 +123,9 @@ hipError_t NoiseSchedule::slot_for(int64_t k, uint64_t seq, Chunk** out) {
   return hipSuccess;
 }
 
-hipError_t NoiseSchedule::upload_done_job(Chunk** out, uint64_t seq) {
+hipError_t NoiseSchedule::upload_done_job(Chunk** out, uint64_t seq, int64_t keep_lo, int64_t keep_hi) {
   Chunk* c = nullptr;
-  hipError_t e = slot_for(job_chunk_, seq, &c);
+  hipError_t e = slot_for(job_chunk_, seq, &c, keep_lo, keep_hi);
   if (e != hipSuccess) return e;
   Stage& s = stage_[job_stage_];
   e = hipMemcpyAsync(c->dev, s.host, kChunkBytes, hipMemcpyHostToDevice, stream_);
@@ -144,12 +145,12 @@ hipError_t NoiseSchedule::upload_done_job(Chunk** out, uint64_t seq) {
   return hipSuccess;
 }
 
-hipError_t NoiseSchedule::poll() {
+hipError_t NoiseSchedule::poll(int64_t keep_lo, int64_t keep_hi) {
   if (!inited_) return hipSuccess;
   std::lock_guard<std::mutex> lk(m_);
   if (job_ != kDone) return hipSuccess;
   Chunk* c = nullptr;
-  return upload_done_job(&c, 0);
+  return upload_done_job(&c, 0, keep_lo, keep_hi);
 }
 
 void NoiseSchedule::prefetch(int64_t k) {

@@ -71,8 +71,13 @@ class NoiseSchedule {
   // Ask the worker to generate chunk k ahead (no-op if it is resident or
   // being generated, or the worker is busy with another chunk).
   void prefetch(int64_t k);
-  // Upload a chunk the worker finished since the last call (async).
-  hipError_t poll();
+  // Upload a chunk the worker finished since the last call (async).  Chunks
+  // [keep_lo, keep_hi] (the ones the caller's draw is about to read) are not
+  // evicted to make room for it.
+  hipError_t poll(int64_t keep_lo = -1, int64_t keep_hi = -2);
+  // Create the upload stream, staging buffers and worker on the current
+  // device (the renderer calls it after hipSetDevice; acquire() otherwise).
+  hipError_t init();
   const Counters& counters() const { return c_; }
 
  private:
@@ -82,12 +87,12 @@ class NoiseSchedule {
     hipEvent_t copied = nullptr;          // the last upload from it
     bool copy_recorded = false;
   };
-  hipError_t init();
   void worker_main();
   void generate(int64_t k, float* out);   // kChunkTables tables on up to 8 host threads
   Chunk* find(int64_t k);
-  hipError_t slot_for(int64_t k, uint64_t seq, Chunk** out);
-  hipError_t upload_done_job(Chunk** out, uint64_t seq);   // job_ is kDone: copy its stage into a chunk (lock held)
+  hipError_t slot_for(int64_t k, uint64_t seq, Chunk** out, int64_t keep_lo = -1, int64_t keep_hi = -2);
+  // job_ is kDone: copy its stage into a chunk (lock held)
+  hipError_t upload_done_job(Chunk** out, uint64_t seq, int64_t keep_lo = -1, int64_t keep_hi = -2);
 
   uint64_t seed_;
   bool static_;

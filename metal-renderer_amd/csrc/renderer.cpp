@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -131,6 +132,10 @@ struct DrawRecord {
   size_t counter_bytes = 0;                 // bytes of `counters` this draw uses
   size_t events = 0;
   bool pending = false;
+  // the counters are all zero once this entry's last draw enqueued its
+  // folding accumulate (which zeroes them behind the draw); a draw that
+  // returned early after its first launch leaves them dirty
+  bool clean = false;
 };
 constexpr int kDrawRing = 3;
 
@@ -151,6 +156,23 @@ struct FrameSlot {
   bool acc_recorded = false;
 };
 
+// Failure state of one RCCL communicator, shared by the communicator and the
+// renderers that enqueued collectives on it (a renderer may outlive it: a
+// deferred unpack after mrt_comm_destroy).  A collective that reports an
+// asynchronous error (ncclCommGetAsyncError) or does not complete within the
+// timeout aborts the communicator (ncclCommAbort: its pending kernels exit);
+// every later use of it fails with MRT_ERR_COMM.  The reference has no
+// collective (one Metal device, renderer/Renderer.mm:595) and ignores its
+// command-buffer errors (:131,141,145); this is the exchange's own contract.
+struct CommHealth {
+  std::mutex m;
+  ncclComm_t comm = nullptr;   // null once destroyed or aborted
+  bool aborted = false;
+  std::string error;           // why it was aborted
+  double timeout_ms = 120000.0;
+  uint32_t inject = 0;         // test entry mrt_debug_comm_fail: 1 async error, 2 collectives never complete
+};
+
 // RCCL communicator of one rank (one process per GPU) and the stream its
 // overlapped collectives run on
 struct mrt_comm {
@@ -158,6 +180,7 @@ struct mrt_comm {
   uint32_t nranks = 0, rank = 0;
   int device = 0;
   hipStream_t stream = nullptr;
+  std::shared_ptr<CommHealth> health = std::make_shared<CommHealth>();
 };
 
 // Image exchange state of a renderer (mrt_renderer_exchange): the packed
@@ -176,6 +199,12 @@ struct Exchange {
   // never dereferences `comm` (it may be destroyed before the flush)
   uint32_t rank = 0, nranks = 1;
   uint32_t width = 0, height = 0;   // image size the pending gather was packed at
+  // the last collective enqueued (on whichever stream it ran) and the health
+  // of its communicator: mrt_renderer_sync / _exchange_flush wait for it with
+  // a bound instead of blocking on a stream a stuck peer never releases
+  hipEvent_t coll_done = nullptr;
+  bool coll_pending = false;
+  std::shared_ptr<CommHealth> health;
 };
 
 struct mrt_renderer {
@@ -299,8 +328,8 @@ int finalize_pending(mrt_renderer* r) {
 // the worker already has) and uploaded asynchronously; never waits for the GPU
 int acquire_noise(mrt_renderer* r, int64_t f0, uint32_t n, std::vector<mrt::NoiseSchedule::Chunk*>* out) {
   using NS = mrt::NoiseSchedule;
-  HIP_TRY(r->noise->poll());
   const int64_t k0 = NS::chunk_of(f0), k1 = NS::chunk_of(f0 + (int64_t)n - 1);
+  HIP_TRY(r->noise->poll(k0, k1));   // (never evicts a chunk this draw reads)
   const uint64_t waits = r->noise->counters().waits;
   for (int64_t k = k0; k <= k1; ++k) {
     NS::Chunk* c = nullptr;
@@ -525,16 +554,86 @@ int exchange_unpack(mrt_renderer* r, int i) {
 // the same buffer runs after it on the communicator's stream, and nothing
 // else reads the buffer), so the overlap of the gather with the next draw
 // is kept.
+int exchange_wait(mrt_renderer* r);
+
 int exchange_drop(mrt_renderer* r, bool wait) {
   Exchange& x = r->x;
   if (x.pending < 0) return MRT_OK;
-  const int i = x.pending;
   x.pending = -1;
-  if (wait) HIP_TRY(hipEventSynchronize(x.gather_done[i]));
+  if (wait) return exchange_wait(r);   // (the pending gather is the last collective)
   return MRT_OK;
 }
 
+// Abort a communicator (lock held): its pending collectives are cancelled
+// and every later use fails.  Returns the MRT_ERR_COMM status.
+int comm_abort_locked(CommHealth& h, const std::string& why) {
+  if (!h.aborted) {
+    if (h.comm) (void)ncclCommAbort(h.comm);
+    h.comm = nullptr;
+    h.aborted = true;
+    h.error = why;
+  }
+  return fail(MRT_ERR_COMM, "RCCL communicator aborted: " + h.error);
+}
+
+// Non-blocking health check of a communicator (lock held).
+int comm_check_locked(CommHealth& h) {
+  if (h.aborted) return fail(MRT_ERR_COMM, "RCCL communicator aborted: " + h.error);
+  if (!h.comm) return MRT_OK;   // destroyed: nothing can fail any more
+  ncclResult_t e = ncclSuccess;
+  if (h.inject == 1) e = ncclSystemError;
+  else if (ncclCommGetAsyncError(h.comm, &e) != ncclSuccess) e = ncclInternalError;
+  if (e != ncclSuccess && e != ncclInProgress)
+    return comm_abort_locked(h, std::string("asynchronous error: ") + ncclGetErrorString(e));
+  return MRT_OK;
+}
+
+// The renderer's exchange state after its communicator failed: nothing is
+// left to unpack or wait for (the image keeps the renderer's own tiles).
+void exchange_forget(mrt_renderer* r) {
+  r->x.pending = -1;
+  r->x.coll_pending = false;
+  r->x.comm = nullptr;
+}
+
+// Wait, with the communicator's timeout as the bound, for the renderer's last
+// collective to complete on the device; poll its asynchronous error meanwhile.
+int exchange_wait(mrt_renderer* r) {
+  Exchange& x = r->x;
+  if (!x.coll_pending) return MRT_OK;
+  std::shared_ptr<CommHealth> h = x.health;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; ++spin) {
+    double timeout_ms;
+    {
+      std::lock_guard<std::mutex> lk(h->m);
+      if (h->inject != 2) {
+        const hipError_t q = hipEventQuery(x.coll_done);
+        if (q == hipSuccess) { x.coll_pending = false; return MRT_OK; }
+        if (q != hipErrorNotReady) {
+          exchange_forget(r);
+          return fail(MRT_ERR_HIP, std::string("exchange: ") + hipGetErrorString(q));
+        }
+      }
+      if (int rc = comm_check_locked(*h)) { exchange_forget(r); return rc; }
+      timeout_ms = h->timeout_ms;
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (ms > timeout_ms) {
+        const int rc = comm_abort_locked(*h, "collective did not complete within " + std::to_string((long)timeout_ms) +
+                                                  " ms (a peer stopped or the link failed)");
+        exchange_forget(r);
+        return rc;
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(spin < 100 ? 20 : 500));
+  }
+}
+
 int exchange_flush(mrt_renderer* r) {
+  if (r->x.coll_pending && r->x.health) {   // a failed communicator surfaces at the next exchange call
+    std::lock_guard<std::mutex> lk(r->x.health->m);
+    if (int rc = comm_check_locked(*r->x.health)) { exchange_forget(r); return rc; }
+  }
   if (r->x.pending < 0) return MRT_OK;
   const int i = r->x.pending;
   r->x.pending = -1;
@@ -1078,6 +1177,13 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
       [&](uint32_t k) { return &scene->occ_tris[12 * (size_t)(k - T)]; }, "occluder tree");
 }
 
+int mrt_debug_magic_div(uint32_t d, const uint32_t* n, uint32_t count, uint32_t* q) {
+  if (d == 0 || (count && (!n || !q))) return fail(MRT_ERR_INVALID, "mrt_debug_magic_div: bad argument");
+  const mrt::MagicDiv m = mrt::magic_div(d);
+  for (uint32_t i = 0; i < count; ++i) q[i] = mrt::mdiv_host(n[i], m);
+  return MRT_OK;
+}
+
 int mrt_debug_box_margin(const mrt_scene* scene, const void* rays, uint32_t stride, uint32_t count,
                          const void* intersections, float* out) {
   if (!scene || (count && (!rays || !intersections || !out))) return fail(MRT_ERR_INVALID, "null argument");
@@ -1402,6 +1508,7 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   r->own_image = desc->image == nullptr;
   r->image = desc->image;
   r->noise = std::make_unique<mrt::NoiseSchedule>(desc->seed, (desc->flags & MRT_FLAG_STATIC_NOISE) != 0);
+  HIP_TRY(r->noise->init());   // its stream and buffers on the renderer's device (set above)
   for (DrawRecord& d : r->draws) {
     HIP_TRY(hipEventCreate(&d.start));
     HIP_TRY(hipEventCreate(&d.stop));
@@ -1597,11 +1704,14 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
   // stream and the draw's other render streams wait for that.
   // The draw's last accumulate copies its statistics to the pinned host copy
   // and zeroes the counters for the ring entry's next draw (whose host side
-  // has waited for that accumulate in finalize_draw): a fresh buffer is the
-  // only one to clear here.  MRT_COUNTER_FOLD=0: memset + copy per draw.
+  // has waited for that accumulate in finalize_draw): a fresh buffer, or one
+  // whose last draw stopped before its folding accumulate, is the only one to
+  // clear here.  MRT_COUNTER_FOLD=0: memset + copy per draw.
   const uint32_t s0 = r->slot_next;
-  if (fresh || !r->counter_fold) HIP_TRY(hipMemsetAsync(d.counters.p, 0, d.counters.bytes, r->slots[s0].stream));
-  if ((fresh || !r->counter_fold) && r->inflight > 1 && nb > 1) {
+  const bool clear = fresh || !d.clean || !r->counter_fold;
+  d.clean = false;   // set again once this draw's folding accumulate is enqueued
+  if (clear) HIP_TRY(hipMemsetAsync(d.counters.p, 0, d.counters.bytes, r->slots[s0].stream));
+  if (clear && r->inflight > 1 && nb > 1) {
     HIP_TRY(hipEventRecord(d.cleared, r->slots[s0].stream));
     for (uint32_t j = 1; j < std::min(nb, r->inflight); ++j)
       HIP_TRY(hipStreamWaitEvent(r->slots[(s0 + j) % r->inflight].stream, d.cleared, 0));
@@ -1643,6 +1753,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.div_tiles = mrt::magic_div(a.tiles_x);
       a.div_slots = mrt::magic_div(a.num_slots);
       a.div_batch = mrt::magic_div(batch);
+      if (!mrt::magic_ok(a.div_tiles, a.tiles_x) || !mrt::magic_ok(a.div_slots, a.num_slots) ||
+          !mrt::magic_ok(a.div_batch, batch))
+        return fail(MRT_ERR_STATE, "draw: a launch divisor's magic multiplier does not divide exactly");
       a.debug = r->debug;
       a.flags = (r->desc.flags & MRT_FLAG_DEBUG_MATERIAL) ? mrt::kShadeDebugMaterial : 0u;
       a.in_segments = 2 * r->grid;   // two material classes per block
@@ -1704,6 +1817,7 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     HIP_TRY(launch_accumulate_frame(r, acc, r->stream));
     HIP_TRY(hipEventRecord(fs.acc_done, r->stream));
     fs.acc_recorded = true;
+    if (k + 1 == nb && r->counter_fold) d.clean = true;
   }
   r->slot_next = (s0 + nb) % r->inflight;
   HIP_TRY(hipEventRecord(d.stop, r->stream));
@@ -1746,7 +1860,11 @@ int mrt_renderer_set_max_frames(mrt_renderer* r, uint32_t max_frames) {
 
 int mrt_renderer_sync(mrt_renderer* r) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");
-  int rc = finalize_pending(r);
+  // the last collective first, with a bound: a stream blocked by a stuck
+  // peer's collective would otherwise hold this host wait forever
+  int rc = exchange_wait(r);
+  if (rc) return rc;
+  rc = finalize_pending(r);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(r->stream));
   return MRT_OK;
@@ -1887,6 +2005,7 @@ int mrt_renderer_stats(const mrt_renderer* r, mrt_stats* stats) {
 
 int mrt_renderer_destroy(mrt_renderer* r) {
   if (!r) return MRT_OK;
+  (void)exchange_wait(r);   // bounded: a failed communicator is aborted, not waited for
   (void)finalize_pending(r);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   for (int i = 0; i < 2; ++i) {   // an overlapped gather may still read the packed tiles
@@ -1894,6 +2013,7 @@ int mrt_renderer_destroy(mrt_renderer* r) {
     if (r->x.pack_done[i]) (void)hipEventDestroy(r->x.pack_done[i]);
     if (r->x.gather_done[i]) (void)hipEventDestroy(r->x.gather_done[i]);
   }
+  if (r->x.coll_done) (void)hipEventDestroy(r->x.coll_done);
   if (r->own_image && r->image) (void)hipFree(r->image);
   for (auto& ds : r->shown) {
     if (ds.done) (void)hipEventDestroy(ds.done);
@@ -1947,6 +2067,7 @@ int mrt_comm_create(const void* id, uint32_t nranks, uint32_t rank, int device, 
     (void)hipStreamDestroy(c->stream);
     return fail(MRT_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(e));
   }
+  c->health->comm = c->comm;
   *out = c.release();
   return MRT_OK;
 }
@@ -1954,10 +2075,35 @@ int mrt_comm_create(const void* id, uint32_t nranks, uint32_t rank, int device, 
 int mrt_comm_destroy(mrt_comm* c) {
   if (!c) return MRT_OK;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  {
+    std::lock_guard<std::mutex> lk(c->health->m);
+    if (c->health->aborted) c->comm = nullptr;   // ncclCommAbort already freed it
+    c->health->comm = nullptr;                   // renderers holding the health no longer touch it
+  }
+  if (c->stream && c->comm) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+  return MRT_OK;
+}
+
+int mrt_comm_set_timeout(mrt_comm* c, uint32_t timeout_ms) {
+  if (!c) return fail(MRT_ERR_INVALID, "null communicator");
+  std::lock_guard<std::mutex> lk(c->health->m);
+  c->health->timeout_ms = timeout_ms ? (double)timeout_ms : 120000.0;
+  return MRT_OK;
+}
+
+int mrt_comm_check(mrt_comm* c) {
+  if (!c) return fail(MRT_ERR_INVALID, "null communicator");
+  std::lock_guard<std::mutex> lk(c->health->m);
+  return comm_check_locked(*c->health);
+}
+
+int mrt_debug_comm_fail(mrt_comm* c, uint32_t mode) {
+  if (!c || mode > 2) return fail(MRT_ERR_INVALID, "mrt_debug_comm_fail: bad argument");
+  std::lock_guard<std::mutex> lk(c->health->m);
+  c->health->inject = mode;
   return MRT_OK;
 }
 
@@ -1972,6 +2118,10 @@ int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
   if (c->nranks != r->desc.shard_count || c->rank != r->desc.shard_rank)
     return fail(MRT_ERR_INVALID, "mrt_renderer_exchange: the renderer's shard (rank, count) must be the comm's");
   if (c->device != r->scene->device) return fail(MRT_ERR_INVALID, "mrt_renderer_exchange: comm on another device");
+  {
+    std::lock_guard<std::mutex> lk(c->health->m);
+    if (int rc = comm_check_locked(*c->health)) return rc;
+  }
   HIP_TRY(hipSetDevice(c->device));
   if (r->x.comm && r->x.comm != c) { int rc = exchange_flush(r); if (rc) return rc; }
   r->x.comm = c;
@@ -1979,8 +2129,12 @@ int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
   if (rc) return rc;
   const uint32_t W = r->desc.width, H = r->desc.height;
   if (c->rank == 0 && c->nranks > 1) r->image_foreign = true;   // other ranks' tiles land in rank 0's image
+  if (!r->x.coll_done) HIP_TRY(hipEventCreateWithFlags(&r->x.coll_done, hipEventDisableTiming));
+  r->x.health = c->health;
   if (kind == MRT_EXCHANGE_REDUCE) {   // one in-place SUM reduce of the RGBA32F image to rank 0
     NCCL_TRY(ncclReduce(r->image, r->image, (size_t)W * H * 4, ncclFloat, ncclSum, 0, c->comm, r->stream));
+    HIP_TRY(hipEventRecord(r->x.coll_done, r->stream));
+    r->x.coll_pending = true;
     return MRT_OK;
   }
   rc = exchange_buffers(r, c);
@@ -2013,12 +2167,16 @@ int mrt_renderer_exchange(mrt_renderer* r, mrt_comm* c, uint32_t mode) {
     }
     NCCL_TRY(ncclGather(x.packed[i].p, recv, x.slab_floats, ncclFloat, 0, c->comm, gs));
     HIP_TRY(hipEventRecord(x.gather_done[i], gs));
+    HIP_TRY(hipEventRecord(x.coll_done, gs));
+    x.coll_pending = true;
     x.gather_recorded[i] = true;
     x.pending = i;
     return MRT_OK;
   }
   NCCL_TRY(ncclGather(x.packed[i].p, recv, x.slab_floats, ncclFloat, 0, c->comm, r->stream));
   HIP_TRY(hipEventRecord(x.gather_done[i], r->stream));
+  HIP_TRY(hipEventRecord(x.coll_done, r->stream));
+  x.coll_pending = true;
   x.gather_recorded[i] = true;
   return exchange_unpack(r, i);
 }
@@ -2059,7 +2217,9 @@ int mrt_debug_exchange_unpack(mrt_renderer* r, uint32_t nranks, const float* gat
 
 int mrt_renderer_exchange_flush(mrt_renderer* r) {
   if (!r) return fail(MRT_ERR_INVALID, "null renderer");
-  return exchange_flush(r);
+  int rc = exchange_flush(r);
+  if (rc) return rc;
+  return exchange_wait(r);   // the collective done on the device, or the communicator aborted
 }
 
 int mrt_renderer_tiles_read(mrt_renderer* r, float* host, size_t floats) {

@@ -52,6 +52,9 @@ class MrtError(RuntimeError):
     pass
 
 
+ERR_COMM = -6   # MRT_ERR_COMM: a collective failed or timed out; the communicator is aborted
+
+
 class SceneDesc(ctypes.Structure):
     _fields_ = [
         ("obj_path", ctypes.c_char_p),
@@ -152,6 +155,7 @@ EXPORTED = [
     "mrt_image_load_exr", "mrt_renderer_load_reference", "mrt_renderer_display",
     "mrt_renderer_display_enqueue", "mrt_renderer_display_map",
     "mrt_debug_lanes", "mrt_debug_exchange_unpack", "mrt_debug_box_margin",
+    "mrt_debug_magic_div", "mrt_comm_set_timeout", "mrt_comm_check", "mrt_debug_comm_fail",
 ]
 
 _lib = None
@@ -207,6 +211,10 @@ def lib() -> ctypes.CDLL:
         "mrt_debug_lanes": [vp, ctypes.c_size_t, c_int],
         "mrt_debug_exchange_unpack": [vp, u32, vp, ctypes.c_size_t],
         "mrt_debug_box_margin": [vp, vp, u32, u32, vp, vp],
+        "mrt_debug_magic_div": [u32, vp, u32, vp],
+        "mrt_comm_set_timeout": [vp, u32],
+        "mrt_comm_check": [vp],
+        "mrt_debug_comm_fail": [vp, u32],
         "mrt_shard_mask": [u32, u32, u32, u32, vp, vp],
         "mrt_tiles_packed_floats": [u32, u32, u32, u32, ctypes.POINTER(u64)],
         "mrt_display": [vp, vp, vp, u32, u32, u32, ctypes.c_float, vp],
@@ -242,7 +250,9 @@ def lib() -> ctypes.CDLL:
 
 def _check(rc: int, what: str) -> None:
     if rc != 0:
-        raise MrtError(f"{what} failed ({rc}): {lib().mrt_last_error().decode()}")
+        e = MrtError(f"{what} failed ({rc}): {lib().mrt_last_error().decode()}")
+        e.status = rc
+        raise e
 
 
 def scene_path(name: str) -> str:
@@ -642,6 +652,16 @@ def tiles_unpack_host(packed, image, rank: int, count: int) -> None:
         image[ty * 64:ty * 64 + h, tx * 64:tx * 64 + w] = packed[k, :h, :w]
 
 
+def debug_magic_div(d: int, n):
+    """n // d through libmrt's exact launch-divisor division (test entry)."""
+    import numpy as np
+    n = np.ascontiguousarray(n, np.uint32)
+    q = np.zeros(len(n), np.uint32)
+    _check(lib().mrt_debug_magic_div(d, ctypes.c_void_p(n.ctypes.data), len(n), ctypes.c_void_p(q.ctypes.data)),
+           "mrt_debug_magic_div")
+    return q
+
+
 def debug_stamps(reset: bool = True):
     import numpy as np
     out = np.zeros(8, np.uint64)
@@ -724,6 +744,18 @@ class Comm:
     @property
     def handle(self):
         return self._h
+
+    def set_timeout(self, ms: int) -> None:
+        """Bound of the renderer's waits for this communicator's collectives (0 = 120 s)."""
+        _check(lib().mrt_comm_set_timeout(self._h, ms), "mrt_comm_set_timeout")
+
+    def check(self) -> None:
+        """Non-blocking health check: raises MrtError once the communicator is aborted."""
+        _check(lib().mrt_comm_check(self._h), "mrt_comm_check")
+
+    def debug_fail(self, mode: int) -> None:
+        """Test entry: 1 = report an asynchronous error, 2 = collectives never complete."""
+        _check(lib().mrt_debug_comm_fail(self._h, mode), "mrt_debug_comm_fail")
 
     def close(self):
         if self._h:

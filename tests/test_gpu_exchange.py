@@ -197,3 +197,53 @@ def test_overlapped_exchange_then_resize_reset_and_comm_close(gpu, mrt_mod):
     r.close()
     ref = _render(mrt_mod, sc, 200, 130, L, frames, 1)
     assert big.tobytes() == ref.tobytes() and after.tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("failure", ["stuck", "async_error"])
+def test_exchange_failure_aborts_communicator(gpu, mrt_mod, failure):
+    """Failure handling of the exchange (SURVEY.md §5 "RCCL async error
+    check"): on a 1-rank communicator the test entry mrt_debug_comm_fail makes
+    the health checks see a collective that never completes (a stuck peer) or
+    an asynchronous RCCL error.  mrt_renderer_sync / _exchange_flush then
+    return MRT_ERR_COMM within the communicator's timeout (bounded wait, not a
+    hang) after a real ncclCommAbort; every later use of the communicator
+    fails cleanly with the same status; the renderer itself keeps rendering;
+    the communicator closes and the process goes on."""
+    import time
+    sc = mrt_mod.Scene("cornellbox")
+    W, H, L = 200, 136, 4
+    comm = mrt_mod.Comm(mrt_mod.comm_unique_id(), 1, 0, 0)
+    comm.set_timeout(300)
+    r = mrt_mod.Renderer(sc, W, H, L)
+    r.draw(2)
+    r.exchange(comm, mrt_mod.EXCHANGE_GATHER | mrt_mod.EXCHANGE_OVERLAP)
+    r.sync()   # healthy: the gather completes, nothing raised
+    comm.check()
+    r.draw(2)
+    r.exchange(comm, mrt_mod.EXCHANGE_GATHER | mrt_mod.EXCHANGE_OVERLAP)
+    comm.debug_fail(2 if failure == "stuck" else 1)
+    t0 = time.time()
+    with pytest.raises(mrt_mod.MrtError) as ei:
+        if failure == "stuck":
+            r.sync()
+        else:
+            r.exchange_flush()
+    dt = time.time() - t0
+    assert ei.value.status == mrt_mod.ERR_COMM, str(ei.value)
+    assert ("did not complete" if failure == "stuck" else "asynchronous error") in str(ei.value)
+    assert dt < 30.0 and (failure != "stuck" or dt >= 0.29), dt
+    # later uses fail cleanly with the same status
+    for call in (comm.check, lambda: r.exchange(comm, mrt_mod.EXCHANGE_GATHER)):
+        with pytest.raises(mrt_mod.MrtError) as ei:
+            call()
+        assert ei.value.status == mrt_mod.ERR_COMM and "aborted" in str(ei.value)
+    # the renderer is unaffected: it renders and reads back its own image
+    r.reset()
+    r.draw(3)
+    img = r.read_image()
+    ref = mrt_mod.Renderer(sc, W, H, L)
+    ref.draw(3)
+    assert img.tobytes() == ref.read_image().tobytes()
+    ref.close()
+    r.close()
+    comm.close()
