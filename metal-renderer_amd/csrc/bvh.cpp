@@ -1,5 +1,6 @@
 // bvh.cpp — binned-SAH BVH2 builder.  See bvh.h.
 #include "bvh.h"
+#include "diag_env.h"
 
 #include <algorithm>
 #include <cfloat>
@@ -321,7 +322,7 @@ bool build_bvh(const float* positions, size_t stride_bytes, const uint32_t* indi
   auto is_leaf = [&](int32_t id) { return bn[id].child[0] < 0; };
   bool dp = opt.collapse_dp > 0 || (opt.collapse_dp < 0 && num_triangles < kGreedyCollapseTriangles);
   if (opt.collapse_dp < 0)
-    if (const char* v = std::getenv("MRT_COLLAPSE")) dp = std::atoi(v) != 0;   // 0: greedy, 1: DP
+    if (const char* v = mrt::diag_env("MRT_COLLAPSE")) dp = std::atoi(v) != 0;   // 0: greedy, 1: DP
   dp = dp && W == 4;
   std::vector<std::array<float, 4>> best;
   std::vector<std::array<uint8_t, 4>> pick;   // k1 of the split (0: m is one slot)

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "diag_env.h"
 #include "kernels.h"
 
 #ifndef MRT_PRECISE
@@ -40,14 +41,6 @@ namespace MRT_NS {
 namespace {
 
 constexpr int kBlock = 256;   // 4 waves of 64 lanes
-#ifndef MRT_SHADE_BARRIERS
-#define MRT_SHADE_BARRIERS 0
-#endif
-#if MRT_SHADE_BARRIERS
-#define MRT_SHADE_BARRIER() __builtin_amdgcn_sched_barrier(0)
-#else
-#define MRT_SHADE_BARRIER() do {} while (0)
-#endif
 // Minimum waves per SIMD for the bounce kernel (launch bounds; the stream
 // kernel has its own, MRT_STREAM_WAVES): 5 caps it at
 // 96 VGPRs with 48 B/lane of scratch spills; 6 (80 VGPRs) spills ~140 B/lane
@@ -104,23 +97,14 @@ __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); 
 // ---------------------------------------------------------------------------
 // Moller-Trumbore, cull none; (u, v) are the weights of (V0, V1) as
 // interpolate() expects (renderer/KernelHelpers.h:37-47).
-// The triangle test's products and sums without FMA contraction
-// (MRT_TRI_NOCONTRACT): the same rounding in every inlined copy of the test —
-// with contraction the compiler may fuse differently per copy, and which copy
-// tests a triangle can depend on how a wave's traversal rounds fall
-#ifndef MRT_TRI_NOCONTRACT
-#define MRT_TRI_NOCONTRACT 0
-#endif
+// The fast build contracts the test's products and sums into FMAs (a
+// no-contraction variant measured slower and was removed in r6); which
+// triangle a near-tie ray reports may then differ from the IEEE answer, never
+// with the visiting order (the culling slack, interior_step).
 __device__ __forceinline__ float tdot(V3 a, V3 b) {
-#if MRT_TRI_NOCONTRACT
-#pragma clang fp contract(off)
-#endif
   return (a.x * b.x + a.y * b.y) + a.z * b.z;
 }
 __device__ __forceinline__ V3 tcross(V3 a, V3 b) {
-#if MRT_TRI_NOCONTRACT
-#pragma clang fp contract(off)
-#endif
   return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 __device__ __forceinline__ bool tri_test(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float tmin, float tmax, float& t,
@@ -170,59 +154,25 @@ struct Hit {
   bool found;
 };
 
-// MRT_NODE_PERM: in the all-in-LDS mode every BVH4 node's x and y plane rows
-// are staged in four copies, one per sign quadrant of (dir.x, dir.y), each
-// pre-ordered (near, far) for rays of that quadrant; a ray reads the copy of
-// its quadrant (and, MRT_ZSEL, its z rows in ray order by a row offset), so
+// Node rows in ray order.  In the all-in-LDS mode every BVH4 node's x and y
+// plane rows are staged in four copies, one per sign quadrant of (dir.x,
+// dir.y), each pre-ordered (near, far) for rays of that quadrant; a ray reads
+// the copy of its quadrant and its z rows in ray order by a row offset, so
 // the box test pairs no planes by min/max (24 fewer VALU ops per node).
-// Slab distances are monotone in the plane coordinate
-// for a fixed direction (in both builds), so the quadrant's near plane is
-// exactly the min of the pair and results are bit-identical.  (Eight octant
-// copies measured -7.5 % on C2: the larger LDS image cost a resident block.)
-#ifndef MRT_NODE_PERM
-#define MRT_NODE_PERM 1
-#endif
-// MRT_ROWSEL: the other modes (top nodes in LDS, the rest in global memory)
-// read a node's plane rows in ray order through per-lane row offsets.
-#ifndef MRT_ROWSEL
-#define MRT_ROWSEL 1
-#endif
-// MRT_ZSEL: the quadrant copy's z rows are also read in ray order (row offsets)
-#ifndef MRT_ZSEL
-#define MRT_ZSEL 1
-#endif
-// MRT_PUSH3: global-memory modes push a node's other hit children with one
-// block of unconditional LDS writes instead of a branch per child
-#ifndef MRT_PUSH3
-#define MRT_PUSH3 0
-#endif
-// MRT_SPILL_FAST: LDS + spill stacks take plain LDS pushes / pops in steps
-// where no lane can reach the spill area (interior_step).  With
-// MRT_BUFFER_NODES: C4 2890 -> 2946 Mpaths/s, C3 2686 -> 2735, C5 1/8 share
-// 1729 -> 1765 (each alone about half of that; r4, alternating in one call)
-#ifndef MRT_SPILL_FAST
-#define MRT_SPILL_FAST 1
-#endif
-// r4 path-kernel instruction diet (A/B in one call, twice each; C4 / C3
-// Mpaths/s): without the two below 2922 / 2752; EMPTY_BOX 3007-3033 /
-// 2818-2823; SPILL_POP_FAST 2971-2976 / 2791-2792
-#ifndef MRT_EMPTY_BOX   // top-nodes mode: empty child slots masked by their inverted box alone (box4 LIVE)
-#define MRT_EMPTY_BOX 1
-#endif
-#ifndef MRT_PUSH3_FAST   // the spill fast path's pushes as three unconditional LDS writes
-#define MRT_PUSH3_FAST 0
-#endif
-#ifndef MRT_TOP_LDS      // top-nodes mode stages the top BVH nodes in LDS (0: every node from memory)
-#define MRT_TOP_LDS 1
-#endif
-#ifndef MRT_SPILL_POP_FAST   // the same for the pops outside interior_step (leaf parking, leaf loop)
-#define MRT_SPILL_POP_FAST 1
-#endif
-// MRT_BUFFER_NODES: global-memory nodes fetched with buffer loads (32-bit
-// offsets from one descriptor: no 64-bit address arithmetic per row)
-#ifndef MRT_BUFFER_NODES
-#define MRT_BUFFER_NODES 1
-#endif
+// Slab distances are monotone in the plane coordinate for a fixed direction
+// (in both builds), so the quadrant's near plane is exactly the min of the
+// pair and results are bit-identical.  (Eight octant copies measured -7.5 %
+// on C2: the larger LDS image cost a resident block.)  The other modes (top
+// nodes in LDS, the rest in global memory) read a node's plane rows in ray
+// order through per-lane row offsets; their empty child slots are masked by
+// their inverted box alone, global nodes are fetched with buffer loads
+// (32-bit offsets from one descriptor), and LDS + spill stacks take plain LDS
+// pushes / pops in steps where no lane can reach the spill area.  r4 A/B
+// (C4 / C3 Mpaths/s, alternating in one call): buffer loads + spill fast
+// path 2890 -> 2946 / 2686 -> 2735; the empty-box mask 3007-3033 / 2818-2823
+// and plain pops 2971-2976 / 2791-2792 against 2922 / 2752 without either.
+// Variants measured slower and removed in r6: unconditional three-entry
+// pushes, an unsorted (slot-order) z row, a no-contraction triangle test.
 constexpr uint32_t kQuadCopies = 4;                      // (x, y) sign quadrants
 constexpr uint32_t kQuadCopyF4 = 7;                      // six plane rows + the refs row
 constexpr uint32_t kQuadNodeF4 = kQuadCopies * kQuadCopyF4;
@@ -265,7 +215,7 @@ __device__ __forceinline__ float slab(float p, float o, float inv, float oinv) {
 // Box test of the four children of a BVH4 node (component-major node, see
 // mrt_layout.h); returns each child's entry distance, +inf for a miss or an
 // empty slot.  ORDERED: the x and y plane rows arrive as (near, far) (a
-// quadrant copy, see MRT_NODE_PERM); otherwise as (lo, hi).
+// quadrant copy of the all-in-LDS mode); otherwise as (lo, hi).
 // LIVE = false (rows in ray order only): empty child slots are not masked by
 // their ref but by their box — the builders store an inverted box (lo = +inf,
 // hi = -inf) in every empty slot, whose near slab is +inf in every ray order
@@ -338,12 +288,12 @@ struct LdsCtx {
 
 __device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
 
-// float4s per staged node: MRT_NODE_PERM (all-in-LDS BVH4 only) stages four
+// float4s per staged node: the all-in-LDS BVH4 stages four
 // quadrant copies of the six plane rows and the refs row (consecutive copies
 // start 28 banks apart, so lanes of different quadrants reading the same node
 // row hit disjoint banks)
 __host__ __device__ constexpr uint32_t node_stride_f4(int mode, uint32_t node_f4) {
-  return (MRT_NODE_PERM && mode == kAllLds && node_f4 == 8) ? kQuadNodeF4 : node_f4;
+  return (mode == kAllLds && node_f4 == 8) ? kQuadNodeF4 : node_f4;
 }
 
 // float4 counts of the staged scene image for a mode
@@ -378,30 +328,24 @@ __device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t rs, uint32_t of
 template <int MODE>
 __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx& cx, int32_t node, const RayBox& rb,
                                             float4* q) {
-  if (MODE == kAllLds && MRT_NODE_PERM) {   // the ray's quadrant copy
-#if MRT_ZSEL
+  if (MODE == kAllLds) {   // the ray's quadrant copy
     const uint32_t sz = fbits(rb.inv.z) >> 31;
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + i];
     q[4] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + 4 + sz];
     q[5] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + 5 - sz];
     q[6] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + 6];
-#else
-#pragma unroll
-    for (int i = 0; i < 7; ++i) q[i] = g_lds[kQuadNodeF4 * node + rb.quad_f4 + i];
-#endif
   } else {
-    // MRT_ROWSEL (top-nodes mode): rows in ray order, (near, far) per axis by the direction's signs
-    const bool rowsel = MRT_ROWSEL && MODE == kTopLds;
+    // top-nodes mode: rows in ray order, (near, far) per axis by the direction's signs
+    const bool rowsel = MODE == kTopLds;
     const uint32_t sx = rowsel ? fbits(rb.inv.x) >> 31 : 0u, sy = rowsel ? fbits(rb.inv.y) >> 31 : 0u;
     const uint32_t sz = rowsel ? fbits(rb.inv.z) >> 31 : 0u;
     const uint32_t row[6] = {sx, 1u - sx, 2u + sy, 3u - sy, 4u + sz, 5u - sz};
-    if (MODE == kAllLds || (MRT_TOP_LDS && MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
+    if (MODE == kAllLds || (MODE == kTopLds && (uint32_t)node < cx.n_lds_nodes)) {
 #pragma unroll
       for (int i = 0; i < 6; ++i) q[i] = g_lds[8 * node + row[i]];
       q[6] = g_lds[8 * node + 6];
     } else {
-#if MRT_BUFFER_NODES
       // one descriptor over the node array (kernel-argument values: wave-
       // uniform); per row a 32-bit offset node * 128 + row * 16
       const __amdgpu_buffer_rsrc_t rs = buf_rsrc(sc.nodes);
@@ -409,12 +353,6 @@ __device__ __forceinline__ void fetch_node4(const DeviceScene& sc, const LdsCtx&
 #pragma unroll
       for (int i = 0; i < 6; ++i) q[i] = buf_ld4(rs, b + (row[i] << 4));
       q[6] = buf_ld4(rs, b + 96u);
-#else
-      const float4* p = reinterpret_cast<const float4*>(sc.nodes) + 8 * (size_t)node;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) q[i] = p[row[i]];
-      q[6] = p[6];
-#endif
     }
   }
 }
@@ -427,18 +365,11 @@ __device__ __forceinline__ void fetch_tri(const DeviceScene& sc, const LdsCtx& c
     t1 = g_lds[cx.tri_base + 3 * k + 1];
     t2 = g_lds[cx.tri_base + 3 * k + 2];
   } else {
-#if MRT_BUFFER_NODES
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(sc.tris);
     const uint32_t b = k * 48u;
     t0 = buf_ld4(rs, b);
     t1 = buf_ld4(rs, b + 16u);
     t2 = buf_ld4(rs, b + 32u);
-#else
-    const float4* p = reinterpret_cast<const float4*>(sc.tris) + 3 * (size_t)k;
-    t0 = p[0];
-    t1 = p[1];
-    t2 = p[2];
-#endif
   }
 }
 
@@ -587,18 +518,6 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 // 2497 Mpaths/s (+28 %), C3 +7.5 %, C3g +5 %, C5 1/8 share +28 % (8 / 16 /
 // 24 / 32 / 48: C4 2456 / 2488 / 2397 / 2281 / 1904).  Shallow all-in-LDS
 // trees lose by it (C2, the stream kernel: slack 2 -1.3 %, 8 -3.4 %).
-#ifndef MRT_CULL_SLACK   // interior_step: cull children only beyond h.t * (1 + 2^-11)
-#define MRT_CULL_SLACK 1
-#endif
-#ifndef MRT_TRAV_SLACK   // traverse(): stream / bounce / stage kernels
-#define MRT_TRAV_SLACK 0
-#endif
-#ifndef MRT_ZERO_NEE   // shade_hit: no shadow query for a light sample of exactly zero
-#define MRT_ZERO_NEE 1
-#endif
-#ifndef MRT_TRAV_LEAF_SLACK   // traverse()'s leaf loop: a lane keeps its untested leaf for the next round
-#define MRT_TRAV_LEAF_SLACK 0
-#endif
 // r4, with the inline shadow finishes (service 32): path slack 8 / 12 / 16
 // C4 2769 / 2852 / 2873, C3 2530 / 2616 / 2660; leaf slack 4 / 8 / 12 C4
 // 2795 / 2852 / 2869, C3 2574 / 2616 / 2638 (one call, alternating)
@@ -611,7 +530,6 @@ constexpr int32_t kDone = 0x7FFFFFFF;   // empty-stack marker
 
 template <int STACK>
 __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
-#if MRT_SPILL_POP_FAST
   // LDS + spill stacks: a plain LDS pop when no active lane's top entry is
   // in the spill area (wave-uniform test)
   if (STACK < 0 && !__any(sp > (STACK < 0 ? -STACK : STACK))) {
@@ -619,7 +537,6 @@ __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
     sp = max(sp - 1, 0);
     return n;
   }
-#endif
   const int32_t n = sp > 0 ? stack_get<STACK>(cx, sp - 1) : kDone;
   sp = max(sp - 1, 0);
   return n;
@@ -649,11 +566,8 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     {
       float4 q[7];
       fetch_node4<MODE>(sc, cx, node, rb, q);
-#if MRT_CULL_SLACK
       tmax *= kCullScale;   // +inf stays +inf
-#endif
-      box4<(MODE == kAllLds && MRT_NODE_PERM) ? (MRT_ZSEL ? 3 : 2) : ((MRT_ROWSEL && MODE == kTopLds) ? 3 : 0),
-           !(MRT_EMPTY_BOX && MRT_ROWSEL && MODE == kTopLds)>(q, o, rb, tmin, tmax, t);
+      box4<MODE == kGlobal ? 0 : 3, MODE != kTopLds>(q, o, rb, tmin, tmax, t);
       r[0] = (int32_t)fbits(q[6].x); r[1] = (int32_t)fbits(q[6].y); r[2] = (int32_t)fbits(q[6].z); r[3] = (int32_t)fbits(q[6].w);
     }
     const float inf = __builtin_inff();
@@ -682,7 +596,6 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
       MRT_CE(0, 1) MRT_CE(0, 2) MRT_CE(0, 3)
     }
 #undef MRT_CE
-#if MRT_SPILL_FAST
     // LDS + spill stacks (deep trees): when no lane of the wave can reach
     // the spill area in this step (sp + 3 <= LDS entries, wave-uniform),
     // the pushes and the pop are plain LDS accesses — no per-entry
@@ -691,19 +604,9 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
     if (STACK < 0 && !__any(sp + 3 > (STACK < 0 ? -STACK : STACK))) {
       constexpr int kL = STACK < 0 ? -STACK : STACK;
       uint32_t* st = lds_u32() + cx.stack_base + threadIdx.x;
-#if MRT_PUSH3_FAST
-      // the hit children after the nearest, far to near, as three
-      // unconditional writes (entries above the new top are garbage)
-      const int c = (int)(t[1] < inf) + (int)(t[2] < inf) + (int)(t[3] < inf);
-      st[sp * kBlock] = (uint32_t)(c == 3 ? r[3] : (c == 2 ? r[2] : r[1]));
-      st[(sp + 1) * kBlock] = (uint32_t)(c == 3 ? r[2] : r[1]);
-      st[(sp + 2) * kBlock] = (uint32_t)r[1];
-      sp += c;
-#else
       if (t[3] < inf) { st[sp * kBlock] = (uint32_t)r[3]; ++sp; }
       if (t[2] < inf) { st[sp * kBlock] = (uint32_t)r[2]; ++sp; }
       if (t[1] < inf) { st[sp * kBlock] = (uint32_t)r[1]; ++sp; }
-#endif
       int32_t next = r[0];
       if (!(t[0] < inf)) {
         next = sp > 0 ? (int32_t)st[(sp - 1) * kBlock] : kDone;
@@ -712,35 +615,6 @@ __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const Ld
       (void)kL;
       return next;
     }
-#endif
-#if MRT_PUSH3
-    if (MODE != kAllLds) {
-      // the hit children after the nearest, far to near, as one block of
-      // three unconditional LDS writes (slots above the new top take
-      // garbage) when the three slots are LDS-resident: no per-child branch
-      const int c = (int)(t[1] < inf) + (int)(t[2] < inf) + (int)(t[3] < inf);
-      const int32_t v0 = c == 3 ? r[3] : (c == 2 ? r[2] : r[1]);
-      const int32_t v1 = c == 3 ? r[2] : r[1];
-      constexpr int kL = STACK < 0 ? -STACK : STACK;
-      if (STACK > 0 || sp + 3 <= kL) {
-        uint32_t* st = lds_u32() + cx.stack_base + threadIdx.x + sp * kBlock;
-        if (STACK > 0 && sp + 3 > kL) {   // full-LDS stacks never overflow: write only the live entries
-          if (c > 0) st[0] = (uint32_t)v0;
-          if (c > 1) st[kBlock] = (uint32_t)v1;
-          if (c > 2) st[2 * kBlock] = (uint32_t)r[1];
-        } else {
-          st[0] = (uint32_t)v0;
-          st[kBlock] = (uint32_t)v1;
-          st[2 * kBlock] = (uint32_t)r[1];
-        }
-      } else {
-        if (c > 0) stack_push<STACK>(cx, sp, v0);
-        if (c > 1) stack_push<STACK>(cx, sp + 1, v1);
-        if (c > 2) stack_push<STACK>(cx, sp + 2, r[1]);
-      }
-      sp += c;
-    } else
-#endif
     {
       if (t[3] < inf) { stack_push<STACK>(cx, sp, r[3]); ++sp; }
       if (t[2] < inf) { stack_push<STACK>(cx, sp, r[2]); ++sp; }
@@ -844,7 +718,7 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
         leaf = node;
         node = stack_pop<STACK>(cx, sp);
       }
-      if ((uint32_t)__popcll(__ballot(leaf == 0)) <= (uint32_t)MRT_TRAV_SLACK) break;
+      if (__ballot(leaf == 0) == 0ull) break;
     }
     // leaves
     while (leaf < 0) {
@@ -858,9 +732,6 @@ __device__ __forceinline__ bool traverse(const DeviceScene& sc, const LdsCtx& cx
         leaf = node;
         node = stack_pop<STACK>(cx, sp);
       }
-#if MRT_TRAV_LEAF_SLACK > 0
-      if ((uint32_t)__popcll(__ballot(leaf < 0)) <= (uint32_t)MRT_TRAV_LEAF_SLACK) break;
-#endif
     }
   }
   return false;
@@ -947,29 +818,18 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
 // this inlined copy of tri_bary differently from the leaf loop's, so on a
 // near-tie (t within an ulp of t_T or 0) the two can disagree; the fast
 // build's 1e-2 image gate covers such flips.  Scenes of >= kOriginTestTriangles only
-// (DeviceScene::origin_test; MRT_ORIGIN_TEST=0 compiles it out).
-#ifndef MRT_ORIGIN_TEST
-#define MRT_ORIGIN_TEST 1
-#endif
+// (DeviceScene::origin_test).
 // the last bounce's occlusion query of a light hit through the occluder tree
 // (shadow_root) instead of the main tree
-#ifndef MRT_LAST_OCC
-#define MRT_LAST_OCC 1
-#endif
 template <int MODE>
 __device__ __forceinline__ bool origin_occludes(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t prim,
                                                 uint32_t target, float tT) {
-#if MRT_ORIGIN_TEST
   if (!sc.origin_test) return false;   // wave-uniform (kernel argument)
   const V3 p0 = mk(fetch_prim<MODE>(sc, cx, prim, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, prim, 1));
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, prim, 2));
   float t, u, v;
   const bool ok = tri_bary(o, d, p0, sub(p1, p0), sub(p2, p0), t, u, v);
   return ok & (prim != target) & (t >= 0.0f) & (t <= tT) & ((t < tT) | (prim < target));
-#else
-  (void)sc; (void)cx; (void)o; (void)d; (void)prim; (void)target; (void)tT;
-  return false;
-#endif
 }
 
 // Shadow-ray resolve under MPS nearest-hit semantics + lightSamplingHandler
@@ -1006,7 +866,7 @@ __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V
 // holds the light hit); false: h.found says whether there is emission.
 // Measured (r4, alternating in one call): C2 (stream kernel) 9738 / 9743 ->
 // 10772 / 10778 Mpaths/s (+10.6 %); the path kernel keeps the full query
-// (MRT_PATH_LAST_LIGHT).
+// (its variant measured C4 -1.3 %, C3 -3.4 %, removed in r6).
 // `graze`: the hit light's cosine to the ray is below the occluder tree's
 // guard (shadow_root; |d . n| / |n| over the geometric normal n = e1 x e2,
 // which occluders.cpp's cos_min covers as it covers the interpolated normal).
@@ -1233,19 +1093,11 @@ __device__ __forceinline__ void slot_pixel(uint32_t s, uint32_t rank, uint32_t c
   y = ty * kTile + (blk >> 3) * 8u + (q >> 3);
 }
 
-#ifndef MRT_MAGIC_DIV
-#define MRT_MAGIC_DIV 1
-#endif
-// n / d for n < 2^31 through the launch's magic (kernels.h MagicDiv), or the
-// plain division (MRT_MAGIC_DIV=0)
+// n / d for n < 2^31 through the launch's magic (kernels.h MagicDiv; draw_n
+// checks every multiplier against its divisor d)
 __device__ __forceinline__ uint32_t mdiv(uint32_t n, MagicDiv m, uint32_t d) {
-#if MRT_MAGIC_DIV
   (void)d;
   return m.m ? (__umulhi(n, m.m) >> m.sh) : n;
-#else
-  (void)m;
-  return n / d;
-#endif
 }
 // slot_pixel with the launch's magic for tiles_x
 __device__ __forceinline__ void slot_pixel_a(uint32_t s, const BounceArgs& a, uint32_t& x, uint32_t& y) {
@@ -1271,7 +1123,7 @@ __device__ __forceinline__ uint32_t shade_noise_cell(uint32_t x, uint32_t y, uin
 // renderer/Shaders.metal:128-211.  Emits the NEE shadow ray (when
 // bounce + 1 < L), adds MIS-weighted emission, and — when `next` — samples
 // the next bounce and updates the throughput.
-template <int MODE, bool SKIP_ZERO = (MRT_ZERO_NEE != 0)>
+template <int MODE, bool SKIP_ZERO = true>
 __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& cx, const Hit& h, PathState& s,
                                           const float4& ns, uint32_t bounce, uint32_t L, bool next, ShadowRay& sh,
                                           bool debug_material) {
@@ -1288,13 +1140,11 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
     light_index = fbits(P1.w);
     hv = add(add(mul(mk(P0), wu), mul(mk(P1), wv)), mul(mk(P2), ww));
   }
-  MRT_SHADE_BARRIER();
   {
     const float4 N0 = fetch_prim<MODE>(sc, cx, h.prim, 3), N1 = fetch_prim<MODE>(sc, cx, h.prim, 4);
     const float4 N2 = fetch_prim<MODE>(sc, cx, h.prim, 5);
     hn = normalize(add(add(mul(mk(N0), wu), mul(mk(N1), wv)), mul(mk(N2), ww)));
   }
-  MRT_SHADE_BARRIER();
   const Mat m = load_material<MODE>(sc, cx, mat_index);
   const V3 wI = s.d;
   if (debug_material) {   // DEBUG_MATERIAL (Shaders.metal:7,142-147): radiance := Fresnel, emission and NEE add to it
@@ -1319,13 +1169,11 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
       lpdf = LB.w;
       lindex = fbits(LD.w);
     }
-    MRT_SHADE_BARRIER();
     {
       const float4 LC = fetch_light<MODE>(sc, cx, li, 2), LE = fetch_light<MODE>(sc, cx, li, 4);
       const float4 LG = fetch_light<MODE>(sc, cx, li, 6);
       ln = normalize(add(add(mul(mk(LC), bu), mul(mk(LE), bv)), mul(mk(LG), bw)));
     }
-    MRT_SHADE_BARRIER();
     const float4 LA = fetch_light<MODE>(sc, cx, li, 0);
     V3 dirToLight;
     float cosL;
@@ -1344,8 +1192,8 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& sc, const LdsCtx& c
     // dielectric pass-through: the material's BSDF is 0 toward the light)
     // changes nothing whether or not it is occluded — R + 0 == R bit for bit,
     // R never being -0 (it starts at +0 and +0 + -0 == +0) — so its shadow
-    // query is not traced (MRT_ZERO_NEE=0, and the B-2 stage kernel, whose
-    // shadow-ray records follow the reference: traced as the reference does)
+    // query is not traced (except by the B-2 stage kernel, whose shadow-ray
+    // records follow the reference: traced as the reference does)
     sh.valid = (lightPdf > 0.0f) && (lindex != h.prim);
     if (SKIP_ZERO) sh.valid = sh.valid && !((sh.L.x == 0.0f) & (sh.L.y == 0.0f) & (sh.L.z == 0.0f));
   }
@@ -1584,7 +1432,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
         Hit hh;
         hh.t = h.t;
         hh.found = false;
-        const int32_t root = MRT_LAST_OCC ? shadow_root(sc, s.o, graze) : sc.root;
+        const int32_t root = shadow_root(sc, s.o, graze);
         if (!(a.debug & 64u) && traverse<STACK, MODE, true>(sc, cx, s.o, s.d, 0.0f, hh, h.prim, root)) h.found = false;
       }
     } else {
@@ -2053,43 +1901,18 @@ __device__ __forceinline__ void trav_round(const DeviceScene& sc, const LdsCtx& 
 #endif
 // Service threshold: finished nearest queries a wave collects before it
 // shades them together.  With finished shadow queries handled inside the
-// traversal loop (MRT_PATH_INLINE_SHADOW, r4) a service round shades 22 of
+// traversal loop (r4) a service round shades 22 of
 // 64 lanes on C3 instead of 16: C4 2803 -> 2849 Mpaths/s (+1.6 %), C3 2491
 // -> 2601 (+4.4 %) at 24, 2848 / 2620 at 32 (16: 2770 / 2471), alternating
 // in one call.
 #ifndef MRT_PATH_SERVICE
 #define MRT_PATH_SERVICE 32
 #endif
-#ifndef MRT_PATH_INLINE_SHADOW
-#define MRT_PATH_INLINE_SHADOW 1
-#endif
-#ifndef MRT_PATH_LAST_LIGHT   // the last-bounce light shortcut (last_bounce_light_hit) in the path kernel
-#define MRT_PATH_LAST_LIGHT 0
-#endif
 
-// Start the nearest query of `bounce` for the lane's ray (ro, rd): phase 1
-// with a full traversal, or on the last bounce with the light shortcut
-// (last_bounce_light_hit) either a finished query at once (no light hit) or
-// phase 3: the occlusion query of the light hit (h keeps it; target = L).
-template <int MODE>
-__device__ __forceinline__ void begin_nearest(const DeviceScene& sc, const LdsCtx& cx, bool last, bool shortcut,
-                                              V3 ro, V3 rd, Hit& h, Trav& tr, uint32_t& phase, uint32_t& target,
-                                              bool& occluded) {
-  if (last && shortcut) {
-    bool graze;
-    if (last_bounce_light_hit<MODE>(sc, cx, ro, rd, h, graze)) {
-      phase = 3;
-      target = h.prim;
-      occluded = false;
-      trav_begin(MRT_LAST_OCC ? shadow_root(sc, ro, graze) : sc.root, tr);
-    } else {
-      phase = 1;
-      tr.node = kDone;
-      tr.leaf = 0;
-      tr.sp = 0;
-    }
-    return;
-  }
+// Start the nearest query of the lane's ray: phase 1, a full traversal.
+// (The last-bounce light shortcut of the wavefront kernels,
+// last_bounce_light_hit, measured C4 -1.3 % / C3 -3.4 % here: removed in r6.)
+__device__ __forceinline__ void begin_nearest(const DeviceScene& sc, Hit& h, Trav& tr, uint32_t& phase) {
   phase = 1;
   trav_begin(sc.root, tr);
   h.t = __builtin_inff(); h.u = h.v = 0.0f; h.prim = 0xFFFFFFFFu; h.found = false;
@@ -2142,10 +1965,6 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
   h.t = 0.0f; h.u = h.v = 0.0f; h.prim = 0u; h.found = false;
   bool occluded = false;
   uint32_t target = 0;
-  // (off by default here: the light test's loads inside the traversal loop
-  // and the service cost more than the 11 % of traversal rounds they save —
-  // C4 3056 vs 3096, C3 2783 vs 2880 Mpaths/s with it, r4)
-  const bool shortcut = MRT_PATH_LAST_LIGHT && sc.light_shortcut && !(a.flags & kShadeDebugMaterial);
 
   for (;;) {
     LS_ADD(25, 1);
@@ -2204,7 +2023,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
           ps[6 * kBlock] = fbits(1.0f); ps[7 * kBlock] = fbits(1.00029f);
           ps[11 * kBlock] = fj * a.num_slots + sl;   // the global slot; prevDiffuse 0
           bounce = 0;
-          begin_nearest<MODE>(sc, cx, L == 1, shortcut, ro, rd, h, tr, phase, target, occluded);
+          begin_nearest(sc, h, tr, phase);
         }
       }
       pool_next += take;
@@ -2214,7 +2033,6 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
     // ---- traversal rounds until enough lanes have finished their query
     bool fin = phase != 0 && trav_done(tr);
     for (;;) {
-#if MRT_PATH_INLINE_SHADOW
       // a finished shadow query needs no shading: its light sample is added
       // (lightSamplingHandler, Shaders.metal:214-231) and the path's next
       // nearest query starts at once, inside the traversal loop, so service
@@ -2230,12 +2048,13 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         bounce += 1;
         atomicAdd(&s_count[bounce - 1], 1u);   // stats: rays alive at the start of this bounce
         rd = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
-        begin_nearest<MODE>(sc, cx, bounce + 1 == L, shortcut, ro, rd, h, tr, phase, target, occluded);
+        begin_nearest(sc, h, tr, phase);
         fin = trav_done(tr);
       }
-#endif
-      // a finished last-bounce occlusion query (phase 3) is the nearest
-      // query's answer: the light hit unless another triangle beat it
+      // (phase 3 — the last-bounce light shortcut's occlusion query — no
+      // longer occurs here; this check of it stays because without it the
+      // compiler allocates the kernel worse: SGPR spills 26 -> 34, scratch
+      // 20 -> 36 B per lane, r6)
       if (fin && phase == 3) {
         h.found = !occluded;
         phase = 1;
@@ -2350,7 +2169,7 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
       atomicAdd(&s_count[bounce - 1], 1u);   // stats: rays alive at the start of this bounce
       // ro already holds the next ray's origin (set at shading, unchanged by a shadow query)
       rd = mk(bitsf(ps[8 * kBlock]), bitsf(ps[9 * kBlock]), bitsf(ps[10 * kBlock]));
-      begin_nearest<MODE>(sc, cx, bounce + 1 == L, shortcut, ro, rd, h, tr, phase, target, occluded);
+      begin_nearest(sc, h, tr, phase);
     }
   }
   __syncthreads();
@@ -2371,16 +2190,8 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
 // its drain (the 2-stream period was launch + ~0.33 ms on C2).  One call,
 // alternating: C2 10755 / 10762 -> 11024 / 11033 Mpaths/s (+2.5 %), C2 L=5
 // +2.0 %, C2 1/8 share 10340 -> 10733 (+3.7 %), C4 +0.5 %.
-#ifndef MRT_ACC_SLIM
-#define MRT_ACC_SLIM 1
-#endif
-#if MRT_ACC_SLIM
 constexpr uint32_t kAccLoads = 4;
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void accumulate_frame_kernel(AccumArgs a) {
-#else
-constexpr uint32_t kAccLoads = 8;
-__global__ __launch_bounds__(kBlock) void accumulate_frame_kernel(AccumArgs a) {
-#endif
   if (a.counters && blockIdx.x == 0) {   // the draw's render launches have completed (stream order)
     for (uint32_t i = threadIdx.x; i < a.copy_words; i += kBlock) a.host_counters[i] = a.counters[i];
     for (uint32_t i = threadIdx.x; i < a.span_words; i += kBlock)
@@ -2525,7 +2336,7 @@ constexpr size_t kAllLdsBudget = 48 * 1024;   // scene bytes staged whole in LDS
 
 int choose_mode(const DeviceScene& sc) {
   static const int forced = [] {   // MRT_MODE=0/1/2 forces kGlobal/kTopLds/kAllLds (profiling)
-    const char* v = std::getenv("MRT_MODE");
+    const char* v = mrt::diag_env("MRT_MODE");
     return v ? std::atoi(v) : -1;
   }();
   if (forced >= 0 && forced <= 2) return forced;
@@ -2599,7 +2410,6 @@ size_t path_lds_bytes(const DeviceScene& sc, int mode, uint32_t stack) {
 DeviceScene fit_path_lds_nodes(const DeviceScene& sc, int mode, uint32_t stack) {
   if (mode != kTopLds) return sc;
   DeviceScene f = sc;
-  if (!MRT_TOP_LDS) { f.lds_nodes = 0; return f; }
   const size_t target = 160 * 1024 / MRT_PATH_WAVES - 2048;
   const size_t fixed = path_lds_bytes(sc, kGlobal, stack) + 64 + 256;   // + static (s_count, s_closed)
   const size_t fit = fixed < target ? (target - fixed) / ((size_t)node_float4s(sc.width) * 16) : 0;

@@ -35,6 +35,7 @@
 #include "occluders.h"
 #include "primary.h"
 #include "scene.h"
+#include "diag_env.h"
 
 namespace {
 
@@ -364,7 +365,7 @@ int alloc_frame_buffers(mrt_renderer* r) {
   // (~19.5 GB at 2^27 rays, of 288 GB).
   const size_t owned_slots = std::max<size_t>(1, (size_t)r->owned_tiles * 4096);
   r->batch = (uint32_t)std::min<size_t>(mrt::kMaxBatch, std::max<size_t>(1, ((size_t)1 << 27) / owned_slots));
-  if (const char* v = std::getenv("MRT_BATCH"))
+  if (const char* v = mrt::diag_env("MRT_BATCH"))
     r->batch = std::max<uint32_t>(1, std::min<uint32_t>(mrt::kMaxBatch, (uint32_t)std::strtoul(v, nullptr, 0)));
   // a ray's tag holds batch * owned slots in 31 bits
   while (r->batch > 1 && owned_slots * r->batch >= ((size_t)1 << 31)) --r->batch;
@@ -781,7 +782,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (desc->lds_nodes == UINT32_MAX) opt.lds_node_budget = 0;
   else if (desc->lds_nodes) opt.lds_node_budget = desc->lds_nodes;
   else opt.lds_node_budget = 256;   // BFS prefix; the launcher stages what fits (fit_lds_nodes)
-  if (const char* v = std::getenv("MRT_LDS_NODES"); v && !desc->lds_nodes) opt.lds_node_budget = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (const char* v = mrt::diag_env("MRT_LDS_NODES"); v && !desc->lds_nodes) opt.lds_node_budget = (uint32_t)std::strtoul(v, nullptr, 0);
   // large scenes (traversed from global memory): a finer SAH — 64 bins, and
   // the exact sweep for ranges below 64 K triangles: C4 1822 -> 1925-1935
   // Mpaths/s (+5.7 %, SAH cost 22.3 -> 20.5), C3 / C3g (7 K triangles) unchanged
@@ -792,12 +793,12 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     opt.bins = 64;
     opt.exact_sah_below = 65536;
   }
-  if (const char* v = std::getenv("MRT_FULL_SWEEP")) opt.full_sweep = std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_FULL_SWEEP")) opt.full_sweep = std::atoi(v) != 0;
   // tuning overrides (profiling): MRT_LEAF = max leaf size, MRT_CTRAV = SAH node cost
-  if (const char* v = std::getenv("MRT_LEAF")) opt.max_leaf_size = (uint32_t)std::strtoul(v, nullptr, 0);
-  if (const char* v = std::getenv("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
-  if (const char* v = std::getenv("MRT_BINS")) opt.bins = (uint32_t)std::strtoul(v, nullptr, 0);
-  if (const char* v = std::getenv("MRT_EXACT_SAH")) opt.exact_sah_below = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (const char* v = mrt::diag_env("MRT_LEAF")) opt.max_leaf_size = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (const char* v = mrt::diag_env("MRT_CTRAV")) opt.traversal_cost = std::strtof(v, nullptr);
+  if (const char* v = mrt::diag_env("MRT_BINS")) opt.bins = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (const char* v = mrt::diag_env("MRT_EXACT_SAH")) opt.exact_sah_below = (uint32_t)std::strtoul(v, nullptr, 0);
   // BVH4 collapse: opt.collapse_dp's size policy (bvh.h), the same for every
   // build path — the area-optimal collapse below 64 K triangles: C2 +0.8 %,
   // C3 +1.9 %, C3g +0.5 %; the 1M-triangle C4 tree (21 % fewer, fuller
@@ -891,7 +892,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   mrt::OccluderSet occ;
   mrt::BvhResult ob;
   bool occ_on = builder == MRT_BVH_HOST_SAH && !desc->no_occluder_tree;
-  if (const char* v = std::getenv("MRT_OCCLUDERS")) occ_on = occ_on && std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_OCCLUDERS")) occ_on = occ_on && std::atoi(v) != 0;
   if (occ_on) {
     std::vector<float> lv, ln;
     for (uint32_t l = 0; l < h.light_count; ++l)
@@ -907,7 +908,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   // light triangles in one wave-uniform loop instead (kernels.hip
   // lights_occlude; MRT_OCC_LIGHTS=0 keeps them in the tree)
   bool occ_lights = occ_on && h.light_count <= mrt::kOccLightsMax;
-  if (const char* v = std::getenv("MRT_OCC_LIGHTS")) occ_lights = occ_lights && std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_OCC_LIGHTS")) occ_lights = occ_lights && std::atoi(v) != 0;
   if (occ_lights) {
     std::vector<uint8_t> is_light(T, 0);
     for (uint32_t l = 0; l < h.light_count; ++l)
@@ -923,9 +924,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     for (uint32_t t : occ.keep) sub.insert(sub.end(), {h.indices[3 * t], h.indices[3 * t + 1], h.indices[3 * t + 2]});
     mrt::BvhBuildOptions oo = opt;
     oo.lds_node_budget = 0;
-    if (const char* v = std::getenv("MRT_OCC_LEAF"))
+    if (const char* v = mrt::diag_env("MRT_OCC_LEAF"))
       oo.max_leaf_size = std::max(1u, std::min<uint32_t>(mrt::kMaxLeafSize, (uint32_t)std::strtoul(v, nullptr, 0)));
-    if (const char* v = std::getenv("MRT_OCC_TCOST")) oo.traversal_cost = std::strtof(v, nullptr);
+    if (const char* v = mrt::diag_env("MRT_OCC_TCOST")) oo.traversal_cost = std::strtof(v, nullptr);
     if (!mrt::build_bvh(h.vertices.data()->v, sizeof(mrt::RefVertex), sub.data(), (uint32_t)occ.keep.size(), oo, ob, err))
       return fail(MRT_ERR_INVALID, "occluder BVH build failed: " + err);
     auto rebase = [&](int32_t r) -> int32_t {
@@ -1019,11 +1020,11 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.width = s->bvh.width;
   d.max_stack = s->bvh.max_stack;
   d.origin_test = T >= mrt::kOriginTestTriangles ? 1u : 0u;   // (global-memory trees)
-  if (const char* v = std::getenv("MRT_ORIGIN_TEST")) d.origin_test = std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_ORIGIN_TEST")) d.origin_test = std::atoi(v) != 0;
   d.region_grabs = T >= mrt::kRegionGrabTriangles ? 1u : 0u;
-  if (const char* v = std::getenv("MRT_REGIONS")) d.region_grabs = std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_REGIONS")) d.region_grabs = std::atoi(v) != 0;
   d.light_shortcut = h.light_count <= mrt::kLightShortcutMax ? 1u : 0u;
-  if (const char* v = std::getenv("MRT_LAST_LIGHT")) d.light_shortcut = d.light_shortcut && std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_LAST_LIGHT")) d.light_shortcut = d.light_shortcut && std::atoi(v) != 0;
   d.occ_root = occ_root;
   d.occ_planes = 0;
   d.occ_lights = 0;
@@ -1146,7 +1147,7 @@ int mrt_scene_check_bvh(const mrt_scene* scene) {
   const mrt::HostScene& h = scene->host;
   const uint32_t T = (uint32_t)h.references.size();
   std::vector<uint8_t> all(T, 1);
-  if (const char* dn = std::getenv("MRT_DUMP_NODE")) {   // diagnostic: one node's rows and its leaf triangles
+  if (const char* dn = mrt::diag_env("MRT_DUMP_NODE")) {   // diagnostic: one node's rows and its leaf triangles
     const uint32_t k = (uint32_t)std::strtoul(dn, nullptr, 0);
     if (k < b.num_nodes) {
       const float* n = &b.nodes[32 * (size_t)k];
@@ -1527,28 +1528,28 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   // may traverse either
   const uint32_t need = desc->scene->dev.max_stack;
   uint32_t cap = need <= 16 ? 16 : (need > 32 ? 12 : 8);
-  if (const char* v = std::getenv("MRT_STACK")) cap = std::max<uint32_t>(8, (uint32_t)std::strtoul(v, nullptr, 0));
+  if (const char* v = mrt::diag_env("MRT_STACK")) cap = std::max<uint32_t>(8, (uint32_t)std::strtoul(v, nullptr, 0));
   const uint32_t want = std::min(need, cap);
   r->stack_entries = want <= 8 ? 8 : want <= 12 ? 12 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
   if (need > r->stack_entries)   // spill variants: 8 / 12 (path kernel; the wavefront runs 16) / 16 / 32
     r->stack_entries = r->stack_entries <= 8 ? 8 : r->stack_entries <= 12 ? 12 : r->stack_entries <= 16 ? 16 : 32;
-  if (const char* dbg = std::getenv("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
-  if (const char* v = std::getenv("MRT_COUNTER_FOLD")) r->counter_fold = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MRT_PROFILE_EVERY"))
+  if (const char* dbg = mrt::diag_env("MRT_DEBUG")) r->debug = (uint32_t)std::strtoul(dbg, nullptr, 0);
+  if (const char* v = mrt::diag_env("MRT_COUNTER_FOLD")) r->counter_fold = std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_PROFILE_EVERY"))
     r->profile_every = std::max<uint32_t>(1, (uint32_t)std::strtoul(v, nullptr, 0));
   {
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, desc->scene->device) == hipSuccess)
       r->wall_khz = (double)khz;
   }
-  if (const char* v = std::getenv("MRT_SPANS"))
+  if (const char* v = mrt::diag_env("MRT_SPANS"))
     if (std::atoi(v) == 0) r->wall_khz = 0.0;
   // two frame batches in flight on their own streams (one launch's drain
   // overlaps the next launch's start): a tile share +5 % (r3.3), a whole C2
   // frame +0.9 % (9598 / 9596 / 9600 vs 9521 / 9479 / 9521 Mpaths/s,
   // alternating in one call)
   r->inflight = 2u;
-  if (const char* v = std::getenv("MRT_INFLIGHT")) r->inflight = (uint32_t)std::strtoul(v, nullptr, 0);
+  if (const char* v = mrt::diag_env("MRT_INFLIGHT")) r->inflight = (uint32_t)std::strtoul(v, nullptr, 0);
   r->inflight = std::max<uint32_t>(1, std::min<uint32_t>(8, r->inflight));
   r->slots.resize(r->inflight);
   for (uint32_t k = 0; k < r->inflight; ++k) {
@@ -1567,15 +1568,15 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   // wavefront), scenes staged whole in LDS the wavefront of per-bounce
   // launches (C2: the path kernel is 24 % slower); MRT_KERNEL=path|wave
   // overrides.
-  if (const char* v = std::getenv("MRT_PRIMARY")) r->primary_allowed = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MRT_PRIMARY_CAP"))
+  if (const char* v = mrt::diag_env("MRT_PRIMARY")) r->primary_allowed = std::atoi(v) != 0;
+  if (const char* v = mrt::diag_env("MRT_PRIMARY_CAP"))
     r->primary_cap = std::max<uint32_t>(1, std::min<uint32_t>(mrt::kPrimaryFallback - 1, (uint32_t)std::strtoul(v, nullptr, 0)));
   r->path_mode = mrt::fast::path_preferred(desc->scene->dev);
-  if (const char* k = std::getenv("MRT_KERNEL")) r->path_mode = std::strcmp(k, "path") == 0;
+  if (const char* k = mrt::diag_env("MRT_KERNEL")) r->path_mode = std::strcmp(k, "path") == 0;
   // streaming wavefront (one launch per frame batch, per-wave ray queues)
   // for whole-scene-in-LDS scenes; MRT_STREAM=0 keeps one launch per bounce
   {
-    const char* c = std::getenv("MRT_STREAM");
+    const char* c = mrt::diag_env("MRT_STREAM");
     const bool want = !c || std::atoi(c) != 0;
     r->stream_allowed = want && !r->path_mode && desc->max_path_length <= mrt::kStreamMaxL &&
                         mrt::fast::stream_supported(desc->scene->dev, r->stack_entries);
@@ -1594,7 +1595,7 @@ int mrt_renderer_create(const mrt_renderer_desc* desc, mrt_renderer** out) {
   else
     HIP_TRY(precise ? mrt::precise::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid)
                     : mrt::fast::bounce_grid(desc->scene->dev, r->stack_entries, 0u, &r->grid));
-  if (const char* g = std::getenv("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
+  if (const char* g = mrt::diag_env("MRT_GRID")) r->grid = std::max<uint32_t>(1, (uint32_t)std::strtoul(g, nullptr, 0));
   int rc = alloc_frame_buffers(r.get());
   if (rc) return rc;
   *out = r.release();

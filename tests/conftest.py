@@ -5,6 +5,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# libmrt honours its diagnostic MRT_* overrides (MRT_INFLIGHT, MRT_BATCH,
+# MRT_KERNEL, ...) only under MRT_DIAG=1; the tests set them
+os.environ["MRT_DIAG"] = "1"
 for sub in ("", "metal-renderer_amd", "oracle", "tests"):
     p = os.path.join(ROOT, sub)
     if p not in sys.path:

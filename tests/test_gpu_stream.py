@@ -71,3 +71,30 @@ def test_stream_with_frames_in_flight(gpu, mrt_mod, monkeypatch, boxes):
     b, sb = _render(mrt_mod, monkeypatch, boxes["cornellbox"], 200, 120, 4, 7, True, False, batch=2, draws=2)
     assert sa["kernel"] == 2 and sb["kernel"] == 2
     assert a.tobytes() == b.tobytes() and sa["active_ray_bounces"] == sb["active_ray_bounces"]
+
+
+def test_stray_kernel_env_ignored_without_mrt_diag(gpu, mrt_mod, monkeypatch):
+    """A stray MRT_KERNEL / MRT_INFLIGHT / MRT_BATCH in the environment does not
+    change the product's kernel choice or streams unless MRT_DIAG=1."""
+    sc = mrt_mod.Scene("cornellbox")
+    monkeypatch.delenv("MRT_DIAG", raising=False)
+    monkeypatch.delenv("MRT_KERNEL", raising=False)
+    monkeypatch.delenv("MRT_INFLIGHT", raising=False)
+    r = mrt_mod.Renderer(sc, 96, 64, 4)
+    want = (r.stats()["kernel"], r.stats()["inflight"])
+    r.draw(2)
+    img = r.read_image()
+    r.close()
+    assert want[0] == 2   # the streaming wavefront for an all-in-LDS scene
+    monkeypatch.setenv("MRT_KERNEL", "wave")
+    monkeypatch.setenv("MRT_INFLIGHT", "3")
+    monkeypatch.setenv("MRT_BATCH", "1")
+    r = mrt_mod.Renderer(sc, 96, 64, 4)
+    assert (r.stats()["kernel"], r.stats()["inflight"]) == want
+    r.draw(2)
+    assert r.read_image().tobytes() == img.tobytes()
+    r.close()
+    monkeypatch.setenv("MRT_DIAG", "1")
+    r = mrt_mod.Renderer(sc, 96, 64, 4)
+    assert (r.stats()["kernel"], r.stats()["inflight"]) == (0, 3)
+    r.close()

@@ -348,3 +348,27 @@ def test_bench_child_argv():
     finally:
         sys.argv = saved
     assert argv[2:] == ["--config", "c5", "--steps", "2", "--gpus", "4"]
+
+
+def test_stray_diagnostic_env_ignored_without_mrt_diag(mrt_mod, monkeypatch):
+    """The library reads its diagnostic MRT_* overrides only under MRT_DIAG=1
+    (csrc/diag_env.h): a host that integrates libmrt with stray variables set
+    gets the product configuration.  Host-only scenes (no device): the BVH
+    builder's and the occluder tree's overrides."""
+    def info():
+        s = mrt_mod.Scene("cornellbox", device=-1)
+        i = dict(s.info)
+        s.close()
+        for k in ("build_ms",):
+            i.pop(k)
+        return i
+    monkeypatch.delenv("MRT_DIAG", raising=False)
+    default = info()
+    assert default["occluder_planes"] > 0
+    for k, v in (("MRT_OCCLUDERS", "0"), ("MRT_LEAF", "8"), ("MRT_COLLAPSE", "0"), ("MRT_BINS", "4"),
+                 ("MRT_KERNEL", "wave"), ("MRT_BATCH", "2"), ("MRT_INFLIGHT", "3")):
+        monkeypatch.setenv(k, v)
+    assert info() == default
+    monkeypatch.setenv("MRT_DIAG", "1")   # the same variables take effect only now
+    diag = info()
+    assert diag["occluder_planes"] == 0 and diag != default

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 # (the bench times them by device spans instead); counters per launch are
 # the same either way
 INF=${MRT_INFLIGHT:-1}
-export MRT_INFLIGHT=$INF
+export MRT_DIAG=1 MRT_INFLIGHT=$INF
 # NAME: the output's config name (default the bench config; e.g. c5s8 for
 # --config c5 --shard-of 8 -> profiles/pmc_c5s8.json via prof_summary.py)
 NAME=${NAME:-$CFG}
@@ -32,9 +32,9 @@ step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -f csv -- $
 # the same run at the renderer's default two render streams: the trace's
 # period per launch (first start to last end of the timed launches / count)
 # is the kernel's share of the step the bench times
-export MRT_INFLIGHT=2
+export MRT_DIAG=1 MRT_INFLIGHT=2
 step trace2 300 rocprofv3 --kernel-trace -d $OUT/trace2 -o run -f csv -- $BENCH
-export MRT_INFLIGHT=$INF
+export MRT_DIAG=1 MRT_INFLIGHT=$INF
 step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/fetch -o run -f csv -- $BENCH
 step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/write -o run -f csv -- $BENCH
 step sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-include-regex 'bounce_|path_kernel|stream_kernel' -d $OUT/sq -o run -f csv -- $BENCH
