@@ -94,7 +94,8 @@ def test_stray_kernel_env_ignored_without_mrt_diag(gpu, mrt_mod, monkeypatch):
     r.draw(2)
     assert r.read_image().tobytes() == img.tobytes()
     r.close()
-    monkeypatch.setenv("MRT_DIAG", "1")
+    monkeypatch.setenv("MRT_DIAG", "1")   # now they apply (MRT_STREAM=0 would select kernel 0 as well)
+    monkeypatch.setenv("MRT_STREAM", "0")
     r = mrt_mod.Renderer(sc, 96, 64, 4)
     assert (r.stats()["kernel"], r.stats()["inflight"]) == (0, 3)
     r.close()
