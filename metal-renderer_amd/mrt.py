@@ -240,6 +240,9 @@ def lib() -> ctypes.CDLL:
         "mrt_renderer_display_map": [vp, u32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)],
     }
     for name, args in sig.items():
+        fn = getattr(L, name, None)
+        if fn is None and os.environ.get("MRT_LIB"):   # an older diagnostic build (A/B): entries it lacks
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = c_int
