@@ -119,6 +119,19 @@ typedef struct mrt_scene_info {
   /* ABI 8: the culled planes (n, w; outward unit normal n, inside
    * n.x - w <= -occluder_margin), occluder_planes of them */
   float occluder_plane[8][4];
+  /* ABI 9: convex occluders — every triangle of the (light-free) occluder
+   * tree lies on one of convex_solids parallelepiped solids (e.g. the Cornell
+   * box's blocks): shadow rays through that tree are decided per solid by a
+   * segment test against its three slabs pushed out by convex_delta, and the
+   * leaf test of the face the segment enters, before any walk (kernels.hip
+   * convex_occlusion).  convex_obb[c] = three unit axis normals (9 floats),
+   * then each axis's padded slab (lo, hi); convex_face_tris[c][2a + side]
+   * (side 0: the lo face, 1: the hi face) = its two primitive ids, 16 bits
+   * each, 0xFFFF = none. */
+  uint32_t convex_solids;
+  float convex_delta;
+  float convex_obb[4][16];
+  uint32_t convex_face_tris[4][8];
 } mrt_scene_info;
 
 int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out);

@@ -792,14 +792,112 @@ __device__ __forceinline__ bool lights_occlude(const DeviceScene& sc, const LdsC
   return occ;
 }
 
+// One face's triangles (conv_face_tris: two primitive ids, 0xFFFF = none)
+// under the leaf test's arithmetic and occlusion rule, as lights_occlude.
+template <int MODE>
+__device__ __forceinline__ bool face_occludes(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t pair,
+                                              uint32_t target, float tT) {
+  bool occ = false;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint32_t prim = (pair >> (16 * j)) & 0xFFFFu;
+    if (prim != 0xFFFFu) {
+      const V3 p0 = mk(fetch_prim<MODE>(sc, cx, prim, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, prim, 1));
+      const V3 p2 = mk(fetch_prim<MODE>(sc, cx, prim, 2));
+      float t, u, v;
+      const bool ok = tri_bary(o, d, p0, sub(p1, p0), sub(p2, p0), t, u, v);
+      occ |= ok & (prim != target) & (t >= 0.0f) & (t <= tT) & ((t < tT) | (prim < target));
+    }
+  }
+  return occ;
+}
+
+// Convex occluders (r6, occluders.h ConvexSet): the occlusion walk of the
+// light samples was ~24 % of the C2 stream kernel (ablation MRT_DEBUG=32:
+// 11.07 -> 8.45 ms per launch), paid per wave for its longest lane.  When
+// every triangle of the occluder tree lies on a convex solid (the Cornell
+// box's two blocks), a lane decides each solid in straight-line code:
+//   * the segment [o, o + t_T d] against the solid's three bounding slabs
+//     pushed out by delta (16x the BVH boxes' padding); an empty interval
+//     means no triangle of the solid can report a hit — the padded-volume
+//     argument the BVH's own culling rests on, with a wider margin;
+//   * a ray that leaves a face of the solid (its shading record's p2.w) with
+//     d . n >= kConvexLeaveCos is separated from the solid by that face's
+//     plane (the origin is 1e-4 outside it, the faces' shading normals are
+//     their plane's, occluders.cpp);
+//   * otherwise the face the segment enters the padded solid through (or, from
+//     inside it, leaves it through) has its triangles leaf-tested with the
+//     occlusion rule: a hit is the traversal's own answer ("occluded"); if
+//     it does not hit, the face the segment leaves through, and then the
+//     solid's other faces — the leaf test over every triangle of the solid,
+//     which is what the walk would have tested.
+// Returns whether a solid occludes; the occluder tree is not walked.
+template <int MODE>
+__device__ __forceinline__ bool convex_occlusion(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
+                                                 float tT, uint32_t origin) {
+  const uint32_t own = fbits(fetch_prim<MODE>(sc, cx, origin, 2).w);   // c * 8 + face + 1 of the origin's solid
+  bool occluded = false;
+  for (uint32_t c = 0; c < sc.conv_count; ++c) {   // wave-uniform; the three slabs unrolled (scalar operands)
+    const float* B = sc.conv_obb[c];
+    float t0 = 0.0f, t1 = tT, own_nd = 0.0f;
+    uint32_t fin = 8u, fout = 8u;   // entry / exit face (2a + side); 8 = none
+#pragma unroll
+    for (uint32_t a = 0; a < 3; ++a) {
+      const float nd = (B[3 * a] * d.x + B[3 * a + 1] * d.y) + B[3 * a + 2] * d.z;
+      const float no = (B[3 * a] * o.x + B[3 * a + 1] * o.y) + B[3 * a + 2] * o.z;
+      const float inv = m_rcp(nd);
+      const float tlo = (B[9 + 2 * a] - no) * inv, thi = (B[10 + 2 * a] - no) * inv;
+      // along +n (the sign bit, so that nd = -0 pairs with inv = -inf): enters
+      // through the lo face, leaves through the hi face; parallel rays get
+      // (-inf, +inf) inside the slab, an empty interval outside, and NaN (no
+      // constraint, the conservative side) exactly on a slab plane
+      const bool pos = (fbits(nd) >> 31) == 0u;
+      const float tn = pos ? tlo : thi, tf = pos ? thi : tlo;
+      const bool in_ = tn > t0, out_ = tf < t1;
+      t0 = in_ ? tn : t0;
+      fin = in_ ? (pos ? 2u * a : 2u * a + 1u) : fin;
+      t1 = out_ ? tf : t1;
+      fout = out_ ? (pos ? 2u * a + 1u : 2u * a) : fout;
+      const uint32_t f0 = c * 8u + 2u * a;
+      own_nd = own == f0 + 1u ? -nd : (own == f0 + 2u ? nd : own_nd);
+    }
+    const bool leaves_own = (own > c * 8u) & (own <= c * 8u + 6u) & (own_nd >= kConvexLeaveCos);
+    if ((t0 <= t1) & !leaves_own & !occluded) {
+      uint32_t pin = 0xFFFFFFFFu, pout = 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t k = 0; k < 6; ++k) {
+        pin = fin == k ? sc.conv_face_tris[c][k] : pin;
+        pout = fout == k ? sc.conv_face_tris[c][k] : pout;
+      }
+      bool hit = face_occludes<MODE>(sc, cx, o, d, pin != 0xFFFFFFFFu ? pin : pout, target, tT);
+      if (!hit & (pin != 0xFFFFFFFFu)) hit = face_occludes<MODE>(sc, cx, o, d, pout, target, tT);
+      // neither face certifies (a near miss within delta, or an entry through
+      // another face near an edge): the solid's other faces, which makes the
+      // lane's answer the leaf test over every triangle of the solid
+      if (!hit) {
+#pragma unroll
+        for (uint32_t k = 0; k < 6; ++k)
+          if (!hit & (k != fin) & (k != fout)) hit = face_occludes<MODE>(sc, cx, o, d, sc.conv_face_tris[c][k], target, tT);
+      }
+      occluded |= hit;
+    }
+  }
+  return occluded;
+}
+
 template <int STACK, int MODE>
 __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                                               float t_target, bool graze) {
+                                               float t_target, bool graze, uint32_t origin) {
   Hit h;
   h.t = t_target;
   h.found = false;
-  const int32_t root = shadow_root(sc, o, graze);
-  if (sc.occ_lights && root == sc.occ_root && lights_occlude<MODE>(sc, cx, o, d, target, t_target)) return true;
+  int32_t root = shadow_root(sc, o, graze);
+  const bool via_occ = root == sc.occ_root;
+  if (sc.conv_count && via_occ) {
+    if (convex_occlusion<MODE>(sc, cx, o, d, target, t_target, origin)) return true;
+    root = kDone;   // no walk (the light triangles are still tested below)
+  }
+  if (sc.occ_lights && via_occ && lights_occlude<MODE>(sc, cx, o, d, target, t_target)) return true;
   return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, root);
 }
 
@@ -846,7 +944,7 @@ __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V
   if (!(tT >= kDistanceEpsilon)) return false;
   if (!(dbg & 128u) && origin_occludes<MODE>(sc, cx, o, d, origin, target, tT)) return false;
   if (dbg & 32u) return true;   // ablation: no occlusion traversal
-  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT, graze);
+  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT, graze, origin);
 }
 
 // Last bounce (bounce + 1 == MAX_PATH_LENGTH): intersectionHandler adds no

@@ -33,6 +33,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <map>
+#include <utility>
 
 namespace mrt {
 
@@ -198,6 +201,153 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
     out = OccluderSet{};
     return false;
   }
+  return true;
+}
+
+bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t num_vertices, const uint32_t* indices,
+                           uint32_t num_triangles, const std::vector<uint32_t>& keep, const OccluderSet& occ,
+                           ConvexSet& out) {
+  out = ConvexSet{};
+  if (keep.empty() || occ.planes.empty() || num_vertices == 0) return false;
+  const size_t stride = stride_bytes / sizeof(float);
+  auto V = [&](uint32_t i) { const float* p = vertices + stride * i; return D3{p[0], p[1], p[2]}; };
+  auto N = [&](uint32_t i) { const float* p = vertices + stride * i + 3; return D3{p[0], p[1], p[2]}; };
+  double amax = 0.0;
+  for (uint32_t i = 0; i < num_vertices; ++i) {
+    const D3 v = V(i);
+    amax = std::max({amax, std::fabs(v.x), std::fabs(v.y), std::fabs(v.z)});
+  }
+  const double S = std::max(amax, 1e-6);
+  const double tol = 1e-6 * S;
+  // corners are matched by position (vertex records are per position and normal)
+  auto key = [&](uint32_t vi) {
+    const float* p = vertices + stride * vi;
+    uint32_t b[3];
+    std::memcpy(b, p, 12);
+    return std::array<uint32_t, 3>{b[0], b[1], b[2]};
+  };
+  std::map<std::array<uint32_t, 3>, uint32_t> pos_id;
+  std::vector<uint32_t> tri_pos(3 * keep.size());
+  for (size_t i = 0; i < keep.size(); ++i)
+    for (int c = 0; c < 3; ++c) {
+      const auto k = key(indices[3 * keep[i] + c]);
+      auto it = pos_id.emplace(k, (uint32_t)pos_id.size()).first;
+      tri_pos[3 * i + c] = it->second;
+    }
+  // connected components over shared positions (union-find)
+  std::vector<uint32_t> parent(pos_id.size());
+  for (size_t i = 0; i < parent.size(); ++i) parent[i] = (uint32_t)i;
+  auto find = [&](uint32_t a) { while (parent[a] != a) a = parent[a] = parent[parent[a]]; return a; };
+  for (size_t i = 0; i < keep.size(); ++i) {
+    const uint32_t a = find(tri_pos[3 * i]);
+    parent[find(tri_pos[3 * i + 1])] = a;
+    parent[find(tri_pos[3 * i + 2])] = find(tri_pos[3 * i]);
+  }
+  std::map<uint32_t, std::vector<size_t>> comps;   // root -> kept-triangle slots
+  for (size_t i = 0; i < keep.size(); ++i) comps[find(tri_pos[3 * i])].push_back(i);
+  if (comps.size() > kMaxConvex) return false;
+  const double delta = 16.0 * (1e-5 * S + 1e-6);   // 16x the BVH boxes' padding (bvh.cpp)
+  out.prim_face.assign(num_triangles, 0u);
+  for (auto& [root, slots] : comps) {
+    (void)root;
+    // the solid's corner positions and centroid
+    std::vector<D3> pts;
+    std::vector<uint8_t> seen(pos_id.size(), 0);
+    D3 cen{0, 0, 0};
+    for (size_t i : slots)
+      for (int c = 0; c < 3; ++c)
+        if (!seen[tri_pos[3 * i + c]]) {
+          seen[tri_pos[3 * i + c]] = 1;
+          const D3 v = V(indices[3 * keep[i] + c]);
+          pts.push_back(v);
+          cen = {cen.x + v.x, cen.y + v.y, cen.z + v.z};
+        }
+    cen = {cen.x / pts.size(), cen.y / pts.size(), cen.z / pts.size()};
+    struct Face { D3 n; double w; std::vector<uint32_t> tris; };
+    std::vector<Face> faces;
+    for (size_t i : slots) {
+      const uint32_t t = keep[i];
+      const D3 v0 = V(indices[3 * t]), v1 = V(indices[3 * t + 1]), v2 = V(indices[3 * t + 2]);
+      const D3 nr = cross(sub(v1, v0), sub(v2, v0));
+      const double a = len(nr);
+      if (!(a > 1e-12 * S * S)) return false;
+      D3 n{nr.x / a, nr.y / a, nr.z / a};
+      double w = dot(n, v0);
+      if (dot(n, cen) - w > 0.0) { n = {-n.x, -n.y, -n.z}; w = -w; }   // outward
+      // flat shading normals: the shadow origin's offset (hit + n_interp * 1e-4)
+      // is then along the face normal
+      for (int c = 0; c < 3; ++c) {
+        const D3 vn = N(indices[3 * t + c]);
+        const double l = len(vn);
+        if (!(l > 0.0) || dot(vn, n) / l < 0.999) return false;
+      }
+      Face* on = nullptr;
+      for (Face& F : faces)
+        if (dot(F.n, n) > 1.0 - 1e-9 && std::fabs(F.w - w) <= tol) { on = &F; break; }
+      if (!on) { faces.push_back(Face{n, w, {}}); on = &faces.back(); }
+      on->tris.push_back(t);
+      if (on->tris.size() > 2) return false;
+    }
+    // the culled planes the solid stands on (its missing faces, e.g. a box's bottom)
+    for (const auto& cp : occ.planes) {
+      const D3 n{cp[0], cp[1], cp[2]};
+      const double w = cp[3];
+      bool touches = false;
+      for (const D3& v : pts) touches |= std::fabs(dot(n, v) - w) <= tol;
+      bool dup = false;
+      for (const Face& F : faces) dup |= dot(F.n, n) > 1.0 - 1e-9 && std::fabs(F.w - w) <= tol;
+      if (touches && !dup) faces.push_back(Face{n, w, {}});
+    }
+    // convex: every corner inside every face plane
+    for (const Face& F : faces)
+      for (const D3& v : pts)
+        if (dot(F.n, v) - F.w > tol) return false;
+    // three pairs of parallel faces (a parallelepiped); axis a's normal is the
+    // first face's of the pair (its "hi" face), the other is the "lo" face
+    if (faces.size() != 6) return false;
+    std::array<float, 16> obb{};
+    std::array<uint32_t, 8> ft;
+    ft.fill(0xFFFFFFFFu);
+    std::vector<uint8_t> used(6, 0);
+    uint32_t axis = 0;
+    auto pack = [&](const Face& F) -> uint32_t {
+      const uint32_t t0 = F.tris.size() > 0 ? F.tris[0] : 0xFFFFu, t1 = F.tris.size() > 1 ? F.tris[1] : 0xFFFFu;
+      return (t0 & 0xFFFFu) | (t1 << 16);
+    };
+    for (size_t i = 0; i < 6 && axis < 3; ++i) {
+      if (used[i]) continue;
+      size_t j = 6;
+      for (size_t k = i + 1; k < 6; ++k)   // the face most nearly opposite (within ~8 degrees)
+        if (!used[k] && dot(faces[i].n, faces[k].n) < -0.99 && (j == 6 || dot(faces[i].n, faces[k].n) <
+                                                                           dot(faces[i].n, faces[j].n)))
+          j = k;
+      if (j == 6) return false;
+      used[i] = used[j] = 1;
+      const Face& H = faces[i];   // n . x <= w_H
+      const Face& L = faces[j];   // -n . x <= w_L  ->  n . x >= -w_L
+      obb[3 * axis] = (float)H.n.x;
+      obb[3 * axis + 1] = (float)H.n.y;
+      obb[3 * axis + 2] = (float)H.n.z;
+      // the slab the solid's corners span along n (the solid's faces need not
+      // be exactly parallel: the Cornell box's blocks are slightly skewed),
+      // [lo - delta, hi + delta] rounded outward: it holds every triangle
+      const D3 na{(double)(float)H.n.x, (double)(float)H.n.y, (double)(float)H.n.z};
+      double lo = 1e300, hi = -1e300;
+      for (const D3& v : pts) { lo = std::min(lo, dot(na, v)); hi = std::max(hi, dot(na, v)); }
+      obb[9 + 2 * axis] = std::nextafter((float)(lo - delta), -INFINITY);
+      obb[9 + 2 * axis + 1] = std::nextafter((float)(hi + delta), INFINITY);
+      for (uint32_t t : L.tris) { if (t >= 0xFFFFu) return false; out.prim_face[t] = out.count * 8 + 2 * axis + 1; }
+      for (uint32_t t : H.tris) { if (t >= 0xFFFFu) return false; out.prim_face[t] = out.count * 8 + 2 * axis + 2; }
+      ft[2 * axis] = pack(L);
+      ft[2 * axis + 1] = pack(H);
+      ++axis;
+    }
+    if (axis != 3) return false;
+    out.obb.push_back(obb);
+    out.face_tris.push_back(ft);
+    out.count += 1;
+  }
+  out.delta = (float)delta;
   return true;
 }
 

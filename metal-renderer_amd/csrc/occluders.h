@@ -43,4 +43,40 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
                     uint32_t num_triangles, const float* light_vertices, const float* light_normals,
                     uint32_t num_lights, OccluderSet& out);
 
+// Convex occluders (r6).  When every triangle of the occluder tree lies on
+// a convex six-faced solid — a connected set of triangles on the faces of
+// the polyhedron their planes bound, three pairs of nearly opposite faces (a
+// face in a culled plane may have no triangles, e.g. a block's bottom on the
+// floor), bounded by the three slabs its corners span along one face normal
+// of each pair —
+// a shadow ray through the occluder tree can be answered without the walk:
+//   * the segment [o, o + t_T d] misses the solid's three bounding slabs
+//     pushed out by `delta`: no triangle of the solid can report a hit (the same
+//     padded-volume argument as the BVH's padded boxes, with a margin 16x
+//     theirs);
+//   * the ray leaves a face of the solid away from it (d . n_face >=
+//     kConvexLeaveCos): the face's plane separates the segment (1e-4 outside
+//     it) from the solid;
+//   * otherwise the leaf test of the triangles of the face the segment enters
+//     (or leaves) the padded solid through, with the leaf test's arithmetic
+//     and acceptance rule, certifies "occluded" exactly; if it does not, the
+//     lane walks the occluder tree as before.
+// Per solid: obb = (n0, n1, n2: unit axis normals, 9 floats; lo_a - delta,
+// hi_a + delta for a = 0..2: 6 floats; 0), face_tris[2a + side] (side 0: the
+// face opposite n_a's, 1: n_a's own face) = its two primitive ids
+// (16 bits each, 0xFFFF = none).  `prim_face[t]` = solid * 8 + 2a + side + 1
+// for the solids' triangles (0 elsewhere): the kernels read it from the
+// primitive's shading record (p2.w).
+struct ConvexSet {
+  uint32_t count = 0;                              // solids (<= kMaxConvex)
+  std::vector<std::array<float, 16>> obb;          // per solid, see above
+  std::vector<std::array<uint32_t, 8>> face_tris;  // per solid: 6 faces (+2 unused, 0xFFFFFFFF)
+  std::vector<uint32_t> prim_face;                 // per scene primitive, see above
+  float delta = 0.0f;
+};
+
+bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t num_vertices, const uint32_t* indices,
+                           uint32_t num_triangles, const std::vector<uint32_t>& keep, const OccluderSet& occ,
+                           ConvexSet& out);
+
 }  // namespace mrt

@@ -964,7 +964,26 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
       s->occ_max_stack = ob.max_stack;
     }
   }
+  // convex occluders (occluders.h): every triangle of the light-free
+  // occluder tree on a convex solid; the solids' faces go to the kernels and
+  // each solid triangle's face index into its shading record (p2.w)
+  mrt::ConvexSet conv;
+  bool conv_on = occ_on && occ_lights && occ_root != mrt::kEmptyChild;
+  if (const char* v = mrt::diag_env("MRT_CONVEX")) conv_on = conv_on && std::atoi(v) != 0;
+  if (conv_on)
+    conv_on = mrt::find_convex_occluders(h.vertices.data()->v, sizeof(mrt::RefVertex), (uint32_t)h.vertices.size(),
+                                         h.indices.data(), T, occ.keep, occ, conv);
+  if (conv_on)
+    for (uint32_t t = 0; t < T; ++t) prims[(size_t)t * 24 + 11] = bitsf(conv.prim_face[t]);
   mrt_scene_info& in = s->info;
+  if (conv_on) {
+    in.convex_solids = conv.count;
+    in.convex_delta = conv.delta;
+    for (uint32_t c = 0; c < conv.count; ++c) {
+      for (int i = 0; i < 16; ++i) in.convex_obb[c][i] = conv.obb[c][i];
+      for (int k = 0; k < 8; ++k) in.convex_face_tris[c][k] = conv.face_tris[c][k];
+    }
+  }
   if (occ_on) {
     in.occluder_planes = (uint32_t)occ.planes.size();
     in.occluder_culled = occ.culled;
@@ -1039,6 +1058,9 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
       for (int c = 0; c < 4; ++c) d.occ_plane[k][c] = occ.planes[k][c];
     d.max_stack = std::max(d.max_stack, ob.max_stack);
   }
+  d.conv_count = in.convex_solids;
+  std::memcpy(d.conv_obb, in.convex_obb, sizeof(d.conv_obb));
+  std::memcpy(d.conv_face_tris, in.convex_face_tris, sizeof(d.conv_face_tris));
   HIP_TRY(alloc_isect_spill(s->isect_spill, d.max_stack));
   in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
   *out = s.release();
@@ -1759,7 +1781,10 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
       a.div_tiles = mrt::magic_div(a.tiles_x);
       a.div_slots = mrt::magic_div(a.num_slots);
       a.div_batch = mrt::magic_div(batch);
-      if (!mrt::magic_ok(a.div_tiles, a.tiles_x) || !mrt::magic_ok(a.div_slots, a.num_slots) ||
+      // (a rank that owns no tile has num_slots 0: its lanes all exit at the
+      // idx < num_slots * batch bound before any quotient by it)
+      if (!mrt::magic_ok(a.div_tiles, a.tiles_x) ||
+          (a.num_slots && !mrt::magic_ok(a.div_slots, a.num_slots)) ||
           !mrt::magic_ok(a.div_batch, batch))
         return fail(MRT_ERR_STATE, "draw: a launch divisor's magic multiplier does not divide exactly");
       a.debug = r->debug;

@@ -101,6 +101,8 @@ class SceneInfo(ctypes.Structure):
         ("occluder_nodes", ctypes.c_uint32), ("occluder_margin", ctypes.c_float),
         ("occluder_max_stack", ctypes.c_uint32), ("occluder_cos_min", ctypes.c_float),
         ("occluder_plane", (ctypes.c_float * 4) * 8),
+        ("convex_solids", ctypes.c_uint32), ("convex_delta", ctypes.c_float),
+        ("convex_obb", (ctypes.c_float * 16) * 4), ("convex_face_tris", (ctypes.c_uint32 * 8) * 4),
     ]
 
 

@@ -287,15 +287,19 @@ def test_gpu_occluder_tree_renders_bitwise(gpu, mrt_mod, monkeypatch, kernel, pr
     the whole scene: images and ray counts bitwise equal with the tree on and
     off, in every kernel (stream, per-bounce, path) and both builds — and with
     the light triangles left out of the tree (tested in lights_occlude, the
-    default) or kept in it (MRT_OCC_LIGHTS=0)."""
+    default) or kept in it (MRT_OCC_LIGHTS=0), and with the convex-occluder
+    test (cornellbox's two blocks, the default there) on and off (MRT_CONVEX=0)."""
     monkeypatch.setenv("MRT_STREAM", "0" if kernel == "bounce" else "1")
     if kernel == "path":
         monkeypatch.setenv("MRT_KERNEL", "path")
     out = []
-    for tree, lights_out in ((True, True), (True, False), (False, True)):
+    for tree, lights_out, convex in ((True, True, True), (True, True, False), (True, False, False),
+                                     (False, True, False)):
         monkeypatch.setenv("MRT_OCC_LIGHTS", "1" if lights_out else "0")
+        monkeypatch.setenv("MRT_CONVEX", "1" if convex else "0")
         s = mrt_mod.Scene(scene, occluder_tree=tree)
         assert (s.info["occluder_planes"] > 0) == tree
+        assert s.info["convex_solids"] == (2 if convex and scene == "cornellbox" else 0)
         r = mrt_mod.Renderer(s, W, H, L, precise=precise)
         r.draw(3)
         out.append((r.read_image(), r.stats()["active_ray_bounces"]))
