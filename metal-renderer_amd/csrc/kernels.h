@@ -109,7 +109,10 @@ struct BounceArgs {
                                //   8 = static interleaved work assignment (no grab counters),
                                //   16 = no material partition of the survivors, 32 = no occlusion traversal
                                //   of light samples, 64 = no occlusion query of last-bounce light hits,
-                               //   128 = no origin-triangle test (stream / bounce kernels)
+                               //   128 = no origin-triangle test (stream / bounce kernels),
+                               //   256 = the accumulate touches no pixel (renderer.cpp draw_n),
+                               //   512 = no convex-occluder test, 1024 = no other-light test (occluder-tree
+                               //   shadow queries, stream / bounce kernels)
   // segmented queues: block g of a launch appends its class-0 survivors
   // (left a diffuse surface) to [g*cap, g*cap + c0_g) and its class-1
   // survivors to [g*cap + cap - c1_g, g*cap + cap) of the output queue

@@ -91,6 +91,11 @@ __device__ __forceinline__ float mixf(float x, float y, float a) { return x + (y
 
 __device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+// set bits of a wave mask in the lanes below this one (v_mbcnt: no per-lane
+// 64-bit mask kept live — in the stream kernel that mask was spilled, r6)
+__device__ __forceinline__ uint32_t lanes_below_in(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
 
 // ---------------------------------------------------------------------------
 // Geometry: MPS nearest-hit semantics (renderer/Renderer.mm:464-469)
@@ -776,11 +781,16 @@ __device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o, bool
 // is unchanged — bit for bit in the precise build; in the fast build the
 // compiler may contract this inlined tri_bary differently from the leaf
 // loop's (as origin_occludes), so a near-tie can flip within the 1e-2 gate.
+// `tl` = the target's light index (its shading record's p1.w): the loop runs
+// num_lights - 1 times, lane by lane over every light but the target (whose
+// test the occlusion rule always rejected) — r6: one test instead of two per
+// C2 shadow ray.
 template <int MODE>
 __device__ __forceinline__ bool lights_occlude(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                                               float tT) {
+                                               uint32_t tl, float tT) {
   bool occ = false;
-  for (uint32_t k = 0; k < sc.num_lights; ++k) {   // wave-uniform
+  for (uint32_t j = 0; j + 1 < sc.num_lights; ++j) {   // wave-uniform trip count
+    const uint32_t k = j < tl ? j : j + 1u;            // per lane: the j-th light other than the target
     const float4 LB = fetch_light<MODE>(sc, cx, k, 1), LD = fetch_light<MODE>(sc, cx, k, 3);
     const float4 LF = fetch_light<MODE>(sc, cx, k, 5);
     const uint32_t prim = fbits(LD.w);
@@ -887,17 +897,18 @@ __device__ __forceinline__ bool convex_occlusion(const DeviceScene& sc, const Ld
 
 template <int STACK, int MODE>
 __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                                               float t_target, bool graze, uint32_t origin) {
+                                               uint32_t tl, float t_target, bool graze, uint32_t origin,
+                                               uint32_t dbg = 0u) {
   Hit h;
   h.t = t_target;
   h.found = false;
   int32_t root = shadow_root(sc, o, graze);
   const bool via_occ = root == sc.occ_root;
   if (sc.conv_count && via_occ) {
-    if (convex_occlusion<MODE>(sc, cx, o, d, target, t_target, origin)) return true;
+    if (!(dbg & 512u) && convex_occlusion<MODE>(sc, cx, o, d, target, t_target, origin)) return true;
     root = kDone;   // no walk (the light triangles are still tested below)
   }
-  if (sc.occ_lights && via_occ && lights_occlude<MODE>(sc, cx, o, d, target, t_target)) return true;
+  if (sc.occ_lights && via_occ && !(dbg & 1024u) && lights_occlude<MODE>(sc, cx, o, d, target, tl, t_target)) return true;
   return traverse<STACK, MODE, true>(sc, cx, o, d, 0.0f, h, target, root);
 }
 
@@ -937,14 +948,15 @@ __device__ __forceinline__ bool origin_occludes(const DeviceScene& sc, const Lds
 template <int STACK, int MODE>
 __device__ bool shadow_reaches_target(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
                                       uint32_t origin, bool graze, uint32_t dbg = 0u) {
-  const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, target, 1));
+  const float4 P1 = fetch_prim<MODE>(sc, cx, target, 1);   // .w: the target's light index
+  const V3 p0 = mk(fetch_prim<MODE>(sc, cx, target, 0)), p1 = mk(P1);
   const V3 p2 = mk(fetch_prim<MODE>(sc, cx, target, 2));
   float tT, u, v;
   if (!tri_test(o, d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v)) return false;
   if (!(tT >= kDistanceEpsilon)) return false;
   if (!(dbg & 128u) && origin_occludes<MODE>(sc, cx, o, d, origin, target, tT)) return false;
   if (dbg & 32u) return true;   // ablation: no occlusion traversal
-  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, tT, graze, origin);
+  return !trace_occluded<STACK, MODE>(sc, cx, o, d, target, fbits(P1.w), tT, graze, origin, dbg);
 }
 
 // Last bounce (bounce + 1 == MAX_PATH_LENGTH): intersectionHandler adds no
@@ -1000,7 +1012,7 @@ __device__ __forceinline__ bool last_bounce_light_hit(const DeviceScene& sc, con
     }
   }
   if (h.found && h.t < kDistanceEpsilon) h.found = false;   // no emission whatever is nearer
-  graze = !(gd >= (sc.occ_cos_min * sc.occ_cos_min) * gn);
+  graze = !(gd >= sc.occ_cos_min2 * gn);
   return h.found;
 }
 
@@ -1465,7 +1477,7 @@ template <int STACK, int MODE, bool WAVEQ = false>
 __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const LdsCtx& cx, const BounceArgs& a,
                                                uint32_t bounce, bool active, uint32_t idx, uint32_t slot,
                                                const RayQueue& in_q, const RayQueue& out_q, uint32_t* cursor,
-                                               uint32_t out_base, uint32_t cap, uint64_t lanes_below,
+                                               uint32_t out_base, uint32_t cap,
                                                StampRef st) {
   const uint32_t lane = threadIdx.x & 63u;
   const bool last = (bounce + 1 == a.max_path_length);
@@ -1600,8 +1612,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
     }
     w0 = __shfl(w0, 0);
     w1 = __shfl(w1, 0);
-    o = cls1 ? out_base + cap - 1u - (w1 + (uint32_t)__popcll(mask1 & lanes_below))
-             : out_base + w0 + (uint32_t)__popcll(mask0 & lanes_below);
+    o = cls1 ? out_base + cap - 1u - (w1 + lanes_below_in(mask1)) : out_base + w0 + lanes_below_in(mask0);
     if (alive && !(a.debug & 4u)) {
       out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
       out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
@@ -1679,7 +1690,6 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
   uint32_t static_base = blockIdx.x * kBlock + (tid & ~63u);
 
   const uint32_t lane = tid & 63u;
-  const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
   STAMP_DECL();
   for (;;) {
@@ -1741,7 +1751,7 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
       }
       STAMP_BEGIN();
       wrote += bounce_wave<STACK, MODE>(sc, cx, a, a.bounce, active, idx, slot, a.in_q, a.out_q, s_cursor,
-                                               out_base, cap, lanes_below, STAMP_REF());
+                                               out_base, cap, STAMP_REF());
     }
     STAMP_WORK();
     if (dynamic && lane == 0) atomicSub(&s_res, kGrab - wrote);
@@ -1808,7 +1818,6 @@ __global__ __launch_bounds__(kBlock, MRT_STREAM_WAVES) void stream_kernel(Device
   const uint32_t N0 = a.num_slots * a.batch;
   const uint32_t rlen = ((N0 + kGrabRanges - 1) / kGrabRanges + kGrab - 1) / kGrab * kGrab;
   uint32_t cur_range = blockIdx.x % kGrabRanges, ranges_left = kGrabRanges;
-  const uint64_t lanes_below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   // this wave's queue: level k (1..L-1) at slots qbase + (k - 1) * kStreamCap
   const uint32_t qbase = (blockIdx.x * (kBlock / 64u) + wave) * (L > 1 ? L - 1 : 1u) * kStreamCap;
   uint32_t pend = 0, pend_end = 0;   // camera rays [pend, pend_end) of the wave's last grab not yet run
@@ -1885,7 +1894,7 @@ __global__ __launch_bounds__(kBlock, MRT_STREAM_WAVES) void stream_kernel(Device
 #endif
     LS_ADD(camera ? 26 : 27, 1);
     const uint32_t wrote = bounce_wave<STACK, MODE, true>(sc, cx, a, camera ? 0u : lvl, active, idx, slot,
-                                                                 a.in_q, a.in_q, nullptr, out, 0u, lanes_below, st);
+                                                                 a.in_q, a.in_q, nullptr, out, 0u, st);
     if (lvl + 1u < L && lane == 0) {
       cnt[lvl + 1u] += wrote;
       s_alive[wave][lvl] += wrote;
@@ -2236,13 +2245,15 @@ __global__ __launch_bounds__(kBlock, MRT_PATH_WAVES) void path_kernel(DeviceScen
         // (MRT_DEBUG bit 1, ablation only: no shadow queries)
         bool shadow = false;
         if (sh.valid && !(a.debug & 1u)) {
-          const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, sh.target, 1));
+          const float4 P1 = fetch_prim<MODE>(sc, cx, sh.target, 1);   // .w: the target's light index
+          const V3 p0 = mk(fetch_prim<MODE>(sc, cx, sh.target, 0)), p1 = mk(P1);
           const V3 p2 = mk(fetch_prim<MODE>(sc, cx, sh.target, 2));
           float tT, u, v;
           const int32_t sroot = shadow_root(sc, ro, sh.graze);
           if (tri_test(ro, sh.d, p0, sub(p1, p0), sub(p2, p0), 0.0f, __builtin_inff(), tT, u, v) &&
               !(tT < kDistanceEpsilon) && !origin_occludes<MODE>(sc, cx, ro, sh.d, h.prim, sh.target, tT) &&
-              !(sc.occ_lights && sroot == sc.occ_root && lights_occlude<MODE>(sc, cx, ro, sh.d, sh.target, tT))) {
+              !(sc.occ_lights && sroot == sc.occ_root &&
+                lights_occlude<MODE>(sc, cx, ro, sh.d, sh.target, fbits(P1.w), tT))) {
             shadow = true;
             phase = 2;
             MRT_TRACE(tagv, "TR S b=%u target=%u tT=%08x root=%d L=%08x %08x %08x\n", bounce, sh.target, fbits(tT),

@@ -124,6 +124,7 @@ struct DeviceScene {
   float occ_cos_min;         // ... and whose cosine to the target light's (interpolated) normal is at least
                              // this (grazing guard for the light's own t error, occluders.cpp)
   float occ_plane[8][4];
+  float occ_cos_min2;        // occ_cos_min squared (host-computed: a loop-invariant VALU product the stream kernel spilled)
   // convex occluders (occluders.h ConvexSet): when every triangle of the
   // occluder tree lies on one of conv_count parallelepiped solids, shadow rays
   // through it are answered by a segment-vs-solid test (kernels.hip

@@ -1054,6 +1054,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     d.occ_planes = (uint32_t)occ.planes.size();
     d.occ_margin = occ.margin;
     d.occ_cos_min = occ.cos_min;
+    d.occ_cos_min2 = occ.cos_min * occ.cos_min;
     for (uint32_t k = 0; k < d.occ_planes; ++k)
       for (int c = 0; c < 4; ++c) d.occ_plane[k][c] = occ.planes[k][c];
     d.max_stack = std::max(d.max_stack, ob.max_stack);
@@ -1833,7 +1834,9 @@ int mrt_renderer_draw_n(mrt_renderer* r, uint32_t n) {
     acc.shard_rank = r->desc.shard_rank;
     acc.shard_count = r->desc.shard_count;
     acc.tiles_x = r->tiles_x;
-    acc.num_slots = r->owned_tiles * 4096u;
+    // (MRT_DEBUG bit 256, ablation: the accumulate launches but touches no
+    // pixel — its statistics fold alone; a wrong image)
+    acc.num_slots = (r->debug & 256u) ? 0u : r->owned_tiles * 4096u;
     acc.radiance = radiance;
     acc.image = reinterpret_cast<float4*>(r->image);
     acc.accumulate = (r->desc.flags & MRT_FLAG_NO_ACCUMULATE) ? 0u : 1u;
