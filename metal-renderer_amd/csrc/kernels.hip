@@ -831,10 +831,21 @@ __device__ __forceinline__ bool face_occludes(const DeviceScene& sc, const LdsCt
 //     pushed out by delta (16x the BVH boxes' padding); an empty interval
 //     means no triangle of the solid can report a hit — the padded-volume
 //     argument the BVH's own culling rests on, with a wider margin;
-//   * a ray that leaves a face of the solid (its shading record's p2.w) with
-//     d . n >= kConvexLeaveCos is separated from the solid by that face's
-//     plane (the origin is 1e-4 outside it, the faces' shading normals are
-//     their plane's, occluders.cpp);
+//   * a ray from a face of a solid (the origin primitive's shading record:
+//     p2.w = its face code, n0.w..n2.w = the face's outward unit normal n)
+//     with d . n >= kConvexLeaveDot (1e-3) skips that solid: n's plane
+//     supports the convex solid and the origin is ~1e-4 outside it (x >=
+//     0.999, the flat shading normal's cosine to n, occluders.cpp), so the
+//     segment moves away from the solid.  The leaf test's error is what
+//     bounds the threshold: a ray grazing an adjacent face's plane near the
+//     shared edge gets barycentrics off by ~u |s| |e| / (|cos| area), so over
+//     3 M adversarial grazing rays from the blocks' faces (70 % within
+//     1e-1 ... 1e-6 of an edge, tilted 1e-1 ... 1e-8 off the face) the largest
+//     d . n of a ray that hits its own solid was 1.0e-5 (IEEE) / -4.2e-5
+//     (FMA): 100x below the threshold (tests/test_convex_occluders.py).
+//     (r6; before, the slab pair's axis normal with d . n >= 0.01: grazing
+//     rays off a block's own face then fell through to the exhaustive test
+//     of its other faces, in 15-20 % of C2's shadow waves at bounces >= 1);
 //   * otherwise the face the segment enters the padded solid through (or, from
 //     inside it, leaves it through) has its triangles leaf-tested with the
 //     occlusion rule: a hit is the traversal's own answer ("occluded"); if
@@ -846,10 +857,13 @@ template <int MODE>
 __device__ __forceinline__ bool convex_occlusion(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
                                                  float tT, uint32_t origin) {
   const uint32_t own = fbits(fetch_prim<MODE>(sc, cx, origin, 2).w);   // c * 8 + face + 1 of the origin's solid
+  const V3 own_n = mk(fetch_prim<MODE>(sc, cx, origin, 3).w, fetch_prim<MODE>(sc, cx, origin, 4).w,
+                      fetch_prim<MODE>(sc, cx, origin, 5).w);   // its face's outward unit normal (0 off the solids)
+  const uint32_t own_skip = ((own != 0u) & (dot(d, own_n) >= kConvexLeaveDot)) ? (own - 1u) >> 3 : 0xFFFFFFFFu;
   bool occluded = false;
   for (uint32_t c = 0; c < sc.conv_count; ++c) {   // wave-uniform; the three slabs unrolled (scalar operands)
     const float* B = sc.conv_obb[c];
-    float t0 = 0.0f, t1 = tT, own_nd = 0.0f;
+    float t0 = 0.0f, t1 = tT;
     uint32_t fin = 8u, fout = 8u;   // entry / exit face (2a + side); 8 = none
 #pragma unroll
     for (uint32_t a = 0; a < 3; ++a) {
@@ -868,10 +882,8 @@ __device__ __forceinline__ bool convex_occlusion(const DeviceScene& sc, const Ld
       fin = in_ ? (pos ? 2u * a : 2u * a + 1u) : fin;
       t1 = out_ ? tf : t1;
       fout = out_ ? (pos ? 2u * a + 1u : 2u * a) : fout;
-      const uint32_t f0 = c * 8u + 2u * a;
-      own_nd = own == f0 + 1u ? -nd : (own == f0 + 2u ? nd : own_nd);
     }
-    const bool leaves_own = (own > c * 8u) & (own <= c * 8u + 6u) & (own_nd >= kConvexLeaveCos);
+    const bool leaves_own = own_skip == c;
     if ((t0 <= t1) & !leaves_own & !occluded) {
       uint32_t pin = 0xFFFFFFFFu, pout = 0xFFFFFFFFu;
 #pragma unroll

@@ -131,17 +131,18 @@ struct DeviceScene {
   // convex_occlusion): conv_obb[c] = three unit axis normals, then each
   // axis's padded slab (lo, hi); conv_face_tris[c][2a + side] = the face's
   // two primitive ids (16 bits each, 0xFFFF = none).  A primitive's shading
-  // record carries (c * 8 + 2a + side + 1) in p2.w (0: not on a solid).
+  // record carries (c * 8 + 2a + side + 1) in p2.w (0: not on a solid) and
+  // its face's outward unit normal in n0.w, n1.w, n2.w.
   uint32_t conv_count;
   float conv_obb[4][16];             // [kMaxConvex]
   uint32_t conv_face_tris[4][8];
 };
 constexpr uint32_t kMaxOccPlanes = 8;
-// convex occluders (DeviceScene::conv_*): solids, face planes in all, and the
-// least cosine between a shadow ray and the face it leaves for that face to
-// separate the ray from its solid (occluders.h)
+// convex occluders (DeviceScene::conv_*): at most this many solids, and the
+// least d . n (n: the outward normal of the face a shadow ray starts on) for
+// the ray to skip that face's solid (kernels.hip convex_occlusion)
 constexpr uint32_t kMaxConvex = 4;
-constexpr float kConvexLeaveCos = 0.01f;
+constexpr float kConvexLeaveDot = 1e-3f;
 // the origin-triangle early-out pays where a shadow ray's descent to its own
 // leaf goes through global memory: measured C4 (1M triangles) +2.6 %, C3
 // (7 K) +0.5 % (with the path kernel's inline shadow finishes), C2 (36, the

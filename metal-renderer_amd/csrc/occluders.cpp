@@ -308,6 +308,7 @@ bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t 
     std::array<float, 16> obb{};
     std::array<uint32_t, 8> ft;
     ft.fill(0xFFFFFFFFu);
+    std::array<float, 18> fn{};
     std::vector<uint8_t> used(6, 0);
     uint32_t axis = 0;
     auto pack = [&](const Face& F) -> uint32_t {
@@ -340,11 +341,17 @@ bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t 
       for (uint32_t t : H.tris) { if (t >= 0xFFFFu) return false; out.prim_face[t] = out.count * 8 + 2 * axis + 2; }
       ft[2 * axis] = pack(L);
       ft[2 * axis + 1] = pack(H);
+      const double ln[3] = {L.n.x, L.n.y, L.n.z}, hn[3] = {H.n.x, H.n.y, H.n.z};
+      for (int c = 0; c < 3; ++c) {
+        fn[3 * (2 * axis) + c] = (float)ln[c];
+        fn[3 * (2 * axis + 1) + c] = (float)hn[c];
+      }
       ++axis;
     }
     if (axis != 3) return false;
     out.obb.push_back(obb);
     out.face_tris.push_back(ft);
+    out.face_normal.push_back(fn);
     out.count += 1;
   }
   out.delta = (float)delta;

@@ -54,9 +54,10 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
 //     pushed out by `delta`: no triangle of the solid can report a hit (the same
 //     padded-volume argument as the BVH's padded boxes, with a margin 16x
 //     theirs);
-//   * the ray leaves a face of the solid away from it (d . n_face >=
-//     kConvexLeaveCos): the face's plane separates the segment (1e-4 outside
-//     it) from the solid;
+//   * the ray leaves the solid's face it starts on, not toward the face's
+//     plane (d . n_face >= 0 over the face's own unit normal, `face_normal`):
+//     the plane — a supporting plane of the convex solid — keeps the whole
+//     segment ~1e-4 outside the solid, beyond the leaf test's reach;
 //   * otherwise the leaf test of the triangles of the face the segment enters
 //     (or leaves) the padded solid through, with the leaf test's arithmetic
 //     and acceptance rule, certifies "occluded" exactly; if it does not, the
@@ -71,6 +72,7 @@ struct ConvexSet {
   uint32_t count = 0;                              // solids (<= kMaxConvex)
   std::vector<std::array<float, 16>> obb;          // per solid, see above
   std::vector<std::array<uint32_t, 8>> face_tris;  // per solid: 6 faces (+2 unused, 0xFFFFFFFF)
+  std::vector<std::array<float, 18>> face_normal;  // per solid: face k's outward unit normal at [3k, 3k+3)
   std::vector<uint32_t> prim_face;                 // per scene primitive, see above
   float delta = 0.0f;
 };

@@ -974,7 +974,13 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
     conv_on = mrt::find_convex_occluders(h.vertices.data()->v, sizeof(mrt::RefVertex), (uint32_t)h.vertices.size(),
                                          h.indices.data(), T, occ.keep, occ, conv);
   if (conv_on)
-    for (uint32_t t = 0; t < T; ++t) prims[(size_t)t * 24 + 11] = bitsf(conv.prim_face[t]);
+    for (uint32_t t = 0; t < T; ++t) {
+      const uint32_t code = conv.prim_face[t];   // c * 8 + face + 1, 0: not on a solid
+      prims[(size_t)t * 24 + 11] = bitsf(code);
+      // the face's outward unit normal in n0.w, n1.w, n2.w (kernels.hip convex_occlusion's own-face test)
+      if (code)
+        for (int c = 0; c < 3; ++c) prims[(size_t)t * 24 + 15 + 4 * c] = conv.face_normal[(code - 1) / 8][3 * ((code - 1) % 8) + c];
+    }
   mrt_scene_info& in = s->info;
   if (conv_on) {
     in.convex_solids = conv.count;

@@ -4,8 +4,8 @@ occluders.h ConvexSet) against the brute-force leaf test, in float32.
 On C2's scene every triangle of the light-free occluder tree lies on one of
 two convex solids (the blocks).  A shadow ray through that tree is decided
 per solid: the segment [o, o + t_T d] against the solid's face planes pushed
-out by delta (Cyrus-Beck); a ray leaving a face of its own solid at
-d . n >= 0.01 skips that solid; otherwise the triangles of the face the
+out by delta (Cyrus-Beck); a ray from a face of a solid with d . n >= 1e-3
+(the face's own outward normal) skips that solid; otherwise the triangles of the face the
 segment enters (or leaves) through are leaf-tested with the occlusion rule,
 and a lane none of them certifies leaf-tests the solid's other faces (so no
 lane walks the occluder tree).
@@ -62,7 +62,7 @@ def _tri_bary(o, d, v0, v1, v2, fma):
     return ok, t
 
 
-def _classify(o, d, tT, own, info, prims, target, fma):
+def _classify(o, d, tT, own, own_n, info, prims, target, fma):
     """kernels.hip convex_occlusion, float32: 1 occluded, 0 clear by the slabs
     or the own face, -1 left to the exhaustive test of a solid (not occluded)."""
     n = len(o)
@@ -70,13 +70,14 @@ def _classify(o, d, tT, own, info, prims, target, fma):
     undecided = np.zeros(n, bool)
     obb = np.array(info["convex_obb"], F)                 # [solid][16]
     pairs = np.array(info["convex_face_tris"], np.uint32)  # [solid][8]
+    # the origin's own solid is skipped when d . n_face >= 1e-3 (its face's own normal, kConvexLeaveDot)
+    own_skip = np.where((own != 0) & (_dot(own_n, d, fma) >= F(1e-3)), (own.astype(np.int64) - 1) >> 3, -1)
     for c in range(info["convex_solids"]):
         B = obb[c]
         t0 = np.zeros(n, F)
         t1 = tT.copy()
         fin = np.full(n, 8, np.uint32)
         fout = np.full(n, 8, np.uint32)
-        own_nd = np.zeros(n, F)
         for a in range(3):
             nv = np.broadcast_to(B[3 * a:3 * a + 3], d.shape)
             nd = _dot(nv, d, fma)
@@ -93,9 +94,7 @@ def _classify(o, d, tT, own, info, prims, target, fma):
             fin = np.where(i_, np.where(pos, 2 * a, 2 * a + 1), fin)
             t1 = np.where(o_, tf, t1)
             fout = np.where(o_, np.where(pos, 2 * a + 1, 2 * a), fout)
-            f0 = c * 8 + 2 * a
-            own_nd = np.where(own == f0 + 1, -nd, np.where(own == f0 + 2, nd, own_nd))
-        leaves_own = (own > c * 8) & (own <= c * 8 + 6) & (own_nd >= F(0.01))
+        leaves_own = own_skip == c
         cand = (t0 <= t1) & ~leaves_own & ~occluded
         pp = np.concatenate([pairs[c], np.full(1, 0xFFFFFFFF, np.uint32)])
         pin, pout = pp[np.minimum(fin, 8)], pp[np.minimum(fout, 8)]
@@ -134,6 +133,34 @@ def _solid_faces(info):
                     own[p] = c * 8 + k + 1
                     solid.append(p)
     return own, sorted(solid)
+
+
+def _face_normals(info, V, tri):
+    """Per primitive: its solid face's outward unit normal (occluders.cpp: the
+    face's first triangle's e1 x e2 in double, turned away from the solid's
+    corner centroid, rounded to float32 — the shading record's n0.w..n2.w);
+    zero off the solids."""
+    pairs = np.array(info["convex_face_tris"], np.uint32)[:info["convex_solids"]]
+    out = np.zeros((len(tri), 3), F)
+    for c in range(pairs.shape[0]):
+        ps = [(int(pairs[c, k]) >> (16 * j)) & 0xFFFF for k in range(6) for j in range(2)]
+        ps = [p for p in ps if p != 0xFFFF]
+        corners = np.unique(V[tri[ps]].reshape(-1, 3).astype(np.float64), axis=0)
+        cen = corners.mean(0)
+        for k in range(6):
+            first = int(pairs[c, k]) & 0xFFFF
+            if first == 0xFFFF:
+                continue
+            v = V[tri[first]].astype(np.float64)
+            nr = np.cross(v[1] - v[0], v[2] - v[0])
+            nr /= np.linalg.norm(nr)
+            if nr @ cen - nr @ v[0] > 0:
+                nr = -nr
+            for j in range(2):
+                p = (int(pairs[c, k]) >> (16 * j)) & 0xFFFF
+                if p != 0xFFFF:
+                    out[p] = nr.astype(F)
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -210,6 +237,7 @@ def test_convex_clear_rays_are_never_hit(mrt_mod, box, fma):
     own_face = np.zeros(len(tri), np.uint32)
     for p, f in own_map.items():
         own_face[p] = f
+    own_normal = _face_normals(info, V, tri)
     for _ in range(14):
         n = 200_000
         o, d, ot, lt = _rays(info, V, N, tri, e, rng, n)
@@ -222,7 +250,7 @@ def test_convex_clear_rays_are_never_hit(mrt_mod, box, fma):
             inside &= (_dot(np.broadcast_to(P[:3], o.shape), o, fma) - P[3]) <= -margin
         keep &= inside
         o, d, ot, lt, tT = o[keep], d[keep], ot[keep], lt[keep], tT[keep]
-        cls = _classify(o, d, tT, own_face[ot], info, prims, lt, fma)
+        cls = _classify(o, d, tT, own_face[ot], own_normal[ot], info, prims, lt, fma)
         # brute force over the blocks' triangles: the occlusion rule
         occ = np.zeros(len(o), bool)
         for t in solid:
@@ -242,3 +270,60 @@ def test_convex_clear_rays_are_never_hit(mrt_mod, box, fma):
     # (adversarial rays: half aimed within 1e-3 ... 1e-7 of a block edge, so
     # far more of them are undecided — left to the exhaustive test — than in a render)
     assert stats["undecided"] <= 0.1 * stats["via_tree"]
+
+
+@pytest.mark.parametrize("fma", [False, True], ids=["ieee", "fma"])
+def test_own_face_grazing_rays_never_hit_their_solid(mrt_mod, box, fma):
+    """The own-face skip (d . n >= 1e-3 over the face's own normal,
+    kConvexLeaveDot) on the rays it is most exposed to: origins on the blocks'
+    faces (offset 1e-4 along the interpolated shading normal, as shade_hit),
+    70 % of them within 1e-1 ... 1e-6 (barycentric) of an edge, directions
+    tangent to the face tilted by +-1e-1 ... 1e-8 along its normal, segments as
+    long as the scene (t_T = 4): no ray that hits its own solid (any triangle
+    the leaf test accepts in [0, t_T]) comes within 10x of the threshold."""
+    info, V, N, tri, e = box
+    prims = V[tri]
+    own_map, solid = _solid_faces(info)
+    normals = _face_normals(info, V, tri)
+    pairs = np.array(info["convex_face_tris"], np.uint32)
+    rng = np.random.default_rng(SEED + 7 + int(fma))
+    worst, hits = -1.0, 0
+    for _ in range(5):
+        n = 200_000
+        ot = rng.choice(solid, n)
+        r1, r2 = rng.random(n).astype(F), rng.random(n).astype(F)
+        edge = rng.random(n) < 0.7
+        r1 = np.where(edge, F(1) - rng.random(n).astype(F) * F(10.0) ** -rng.uniform(1, 6, n).astype(F), r1)
+        sq = np.sqrt(r1).astype(F)
+        w = np.stack([F(1) - sq, sq * (F(1) - r2), sq * r2], 1).astype(F)
+        w = np.take_along_axis(w, rng.permuted(np.tile(np.arange(3), (n, 1)), axis=1), 1)
+        v, nv = V[tri[ot]], N[tri[ot]]
+        hv = (v[:, 0] * w[:, :1] + v[:, 1] * w[:, 1:2] + v[:, 2] * w[:, 2:]).astype(F)
+        hn = (nv[:, 0] * w[:, :1] + nv[:, 1] * w[:, 1:2] + nv[:, 2] * w[:, 2:]).astype(F)
+        hn = (hn / np.sqrt((hn * hn).sum(1, keepdims=True))).astype(F)
+        o = (hv + hn * F(1e-4)).astype(F)
+        fn = normals[ot].astype(np.float64)
+        tan = rng.standard_normal((n, 3))
+        tan -= (tan * fn).sum(1, keepdims=True) * fn
+        tan /= np.linalg.norm(tan, axis=1, keepdims=True)
+        tilt = rng.choice([-1.0, 1.0], n) * 10.0 ** -rng.uniform(1, 8, n)
+        d = (tan + tilt[:, None] * fn)
+        d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(F)
+        nd = _dot(normals[ot], d, fma)
+        c_own = np.array([(own_map[int(p)] - 1) >> 3 for p in ot])
+        hit = np.zeros(n, bool)
+        for c in range(info["convex_solids"]):
+            mine = c_own == c
+            for k in range(6):
+                for j in range(2):
+                    p = (int(pairs[c, k]) >> (16 * j)) & 0xFFFF
+                    if p == 0xFFFF:
+                        continue
+                    ok, t = _tri_bary(o, d, prims[p, 0], prims[p, 1], prims[p, 2], fma)
+                    hit |= mine & ok & (t >= 0) & (t <= F(4.0))
+        hits += int(hit.sum())
+        if hit.any():
+            worst = max(worst, float(nd[hit].max()))
+    print(dict(hits=hits, worst_dot=worst))
+    assert hits > 10_000                 # the sample reaches its solid often (rays tilted into it)
+    assert worst < 1e-4                  # 10x below kConvexLeaveDot = 1e-3
