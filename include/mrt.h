@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 10
+#define MRT_ABI_VERSION 9
 
 typedef enum mrt_status {
   MRT_OK = 0,
@@ -132,20 +132,6 @@ typedef struct mrt_scene_info {
   float convex_delta;
   float convex_obb[4][16];
   uint32_t convex_face_tris[4][8];
-  /* ABI 10: nearest queries from inside the room (kernels.hip room_nearest):
-   * when every triangle is a light, a culled wall triangle or on a convex
-   * solid, a path ray whose origin is inside every culled plane is answered
-   * without a tree walk — per solid the faces whose own padded extent the ray
-   * crosses inside the padded solid (convex_inner[c][2a] = the lo face's reach
-   * along axis a, [2a + 1] = the hi face's; convex_near_tris = face pairs
-   * with the bottoms filled in), the culled planes it can leave the room
-   * through (wall_pairs[k] = plane k's triangles, two 16-bit ids per word,
-   * 0xFFFF = none), and every light triangle.  room_nearest = 0: off. */
-  uint32_t room_nearest;
-  float room_graze;                /* |cos| to a culled plane below which its triangles are always tested */
-  float convex_inner[4][6];
-  uint32_t convex_near_tris[4][6];
-  uint32_t wall_pairs[8][2];
 } mrt_scene_info;
 
 int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out);

@@ -17,7 +17,7 @@ namespace mrt {
 //   plane 0: (origin.xyz, bits(slot | prevDiffuse << 31))    = Ray.origin, params.y
 //            slot = frame_in_batch * num_slots + owned slot (the pixel's
 //            radiance index; the pixel is decoded from it, kernels.hip)
-//   plane 1: (direction.xyz, bits(the primitive it leaves))  = Ray.direction
+//   plane 1: (direction.xyz, 0)                            = Ray.direction
 //   plane 2: (throughput.rgb, material pdf)                = Ray.throughput, params.x
 //   plane 3: (radiance.rgb, ior)                           = Ray.radiance, params.w
 // Planes 0-1 are all the traversal needs; planes 2-3 are loaded after the
@@ -112,8 +112,7 @@ struct BounceArgs {
                                //   128 = no origin-triangle test (stream / bounce kernels),
                                //   256 = the accumulate touches no pixel (renderer.cpp draw_n),
                                //   512 = no convex-occluder test, 1024 = no other-light test (occluder-tree
-                               //   shadow queries, stream / bounce kernels), 2048 = no room_nearest (the
-                               //   tree walk instead; same image)
+                               //   shadow queries, stream / bounce kernels)
   // segmented queues: block g of a launch appends its class-0 survivors
   // (left a diffuse surface) to [g*cap, g*cap + c0_g) and its class-1
   // survivors to [g*cap + cap - c1_g, g*cap + cap) of the output queue

@@ -761,17 +761,14 @@ __device__ __forceinline__ Hit trace_nearest(const DeviceScene& sc, const LdsCtx
 // light's plane (`graze`: cosine below occ_cos_min, where the light's own t
 // error could reach a culled crossing), else the main tree.  The plane data
 // is wave-uniform (kernel argument, scalar registers).
-__device__ __forceinline__ bool inside_room(const DeviceScene& sc, V3 o) {
+__device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o, bool graze) {
+  if (sc.occ_planes == 0 || graze) return sc.root;
   bool inside = true;
   for (uint32_t k = 0; k < sc.occ_planes; ++k) {
     const float* p = sc.occ_plane[k];
     inside &= fmaf(p[0], o.x, fmaf(p[1], o.y, fmaf(p[2], o.z, -p[3]))) <= -sc.occ_margin;
   }
-  return inside;
-}
-__device__ __forceinline__ int32_t shadow_root(const DeviceScene& sc, V3 o, bool graze) {
-  if (sc.occ_planes == 0 || graze) return sc.root;
-  return inside_room(sc, o) ? sc.occ_root : sc.root;
+  return inside ? sc.occ_root : sc.root;
 }
 
 // The light triangles of an occluder tree built without them (DeviceScene::
@@ -908,200 +905,6 @@ __device__ __forceinline__ bool convex_occlusion(const DeviceScene& sc, const Ld
     }
   }
   return occluded;
-}
-
-// One face's (or wall's) triangle pair under the leaf test's arithmetic and
-// the nearest-hit tie rule (tri_pair's: t in [0, h.t], ties to the lowest
-// primitive); `pair` = two 16-bit primitive ids, 0xFFFF = none.
-template <int MODE>
-__device__ __forceinline__ void pair_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t pair,
-                                             Hit& h) {
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const uint32_t prim = (pair >> (16 * j)) & 0xFFFFu;
-    if (prim != 0xFFFFu) {
-      const V3 p0 = mk(fetch_prim<MODE>(sc, cx, prim, 0)), p1 = mk(fetch_prim<MODE>(sc, cx, prim, 1));
-      const V3 p2 = mk(fetch_prim<MODE>(sc, cx, prim, 2));
-      float t, u, v;
-      const bool ok = tri_bary(o, d, p0, sub(p1, p0), sub(p2, p0), t, u, v);
-      const bool hit = ok & (t >= 0.0f) & (t <= h.t);
-      if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
-        h.found = true;
-        h.t = t;
-        h.u = u;
-        h.v = v;
-        h.prim = prim;
-      }
-    }
-  }
-}
-
-// Nearest queries from inside the room without a tree walk (r6,
-// DeviceScene::room_nearest, renderer.cpp): every triangle is a light, a
-// wall triangle of one culled plane, or on one of the convex solids
-// (occluders.h ConvexSet, bottoms included), and the ray's origin is inside
-// every culled plane by occ_margin.  The answer is the nearest (t, prim) over
-// a candidate set that holds every triangle the leaf test could accept at
-// t <= the answer, each tested with the leaf test's arithmetic and tie rule
-// (tri_bary over the shading record's vertices: the leaf record's v0, e1, e2
-// bit for bit), so it is the traversal's (precise build: bitwise):
-//   * solids: a solid's face triangles lie in the face's padded region — its
-//     own reach along its axis (conv_inner: a skewed solid's faces are not
-//     quite perpendicular to the axis) padded by delta, times the other two
-//     axes' padded slabs — the BVH's padded-volume argument with 16x its
-//     margin, on an oriented box.  A face is a candidate when the ray is
-//     inside its region while inside the solid's padded box, no later than
-//     h.t (1 + 2^-11) (interior_step's culling slack).  The face the ray
-//     enters through is tested first; the others (the exit face, culled by
-//     that hit; faces near an edge) after it.  A ray starting on a solid's
-//     face and leaving it (d . n >= kConvexLeaveDot, as convex_occlusion)
-//     skips that solid.
-//   * walls: the culled planes are supporting planes of the scene and the
-//     origin is inside them, so past the first t at which the ray is Delta
-//     outside an approached plane (t_hi) it is Delta from every wall; a wall
-//     is a candidate when its padded crossing [t_lo, t_hi] starts before
-//     that bound and h.t (1 + 2^-11), or when the ray approaches its plane at
-//     |cos| < room_graze (the leaf test's error grows as 1 / |cos|).
-//     Planes the ray moves away from cannot report t >= 0 (the origin is
-//     inside by occ_margin, above the test's error, occluders.cpp).
-//   * every light triangle.
-// CPU-checked in the kernels' float32 arithmetic against the brute force
-// (tests/test_room_nearest.py); `origin` = the primitive the ray leaves.
-template <int MODE>
-__device__ __forceinline__ void room_nearest(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t origin,
-                                             Hit& h) {
-  h.t = __builtin_inff();
-  h.u = h.v = 0.0f;
-  h.prim = 0xFFFFFFFFu;
-  h.found = false;
-  uint32_t own_skip = 0xFFFFFFFFu;   // the solid the ray starts on and leaves
-  if (origin < sc.num_triangles) {
-    const uint32_t own = fbits(fetch_prim<MODE>(sc, cx, origin, 2).w);
-    const V3 own_n = mk(fetch_prim<MODE>(sc, cx, origin, 3).w, fetch_prim<MODE>(sc, cx, origin, 4).w,
-                        fetch_prim<MODE>(sc, cx, origin, 5).w);
-    own_skip = ((own != 0u) & (dot(d, own_n) >= kConvexLeaveDot)) ? (own - 1u) >> 3 : 0xFFFFFFFFu;
-  }
-  // -- solids
-  for (uint32_t c = 0; c < sc.conv_count; ++c) {   // wave-uniform; axes unrolled (scalar operands)
-    const float* B = sc.conv_obb[c];
-    const float* I = sc.conv_inner[c];
-    float T0 = 0.0f, T1 = h.t * kCullScale;   // +inf stays +inf
-    float e0[3], e1[3], x0[3], x1[3];          // entering / leaving face region per axis
-    uint32_t neg = 0u;                         // bit a: the ray runs along -n_a (enters the hi face)
-#pragma unroll
-    for (uint32_t a = 0; a < 3; ++a) {
-      const float nd = (B[3 * a] * d.x + B[3 * a + 1] * d.y) + B[3 * a + 2] * d.z;
-      const float no = (B[3 * a] * o.x + B[3 * a + 1] * o.y) + B[3 * a + 2] * o.z;
-      const float inv = m_rcp(nd);
-      const float tl = (B[9 + 2 * a] - no) * inv, th = (B[10 + 2 * a] - no) * inv;
-      const float til = (I[2 * a] - no) * inv, tih = (I[2 * a + 1] - no) * inv;
-      // along +n (the sign bit, as convex_occlusion) the ray enters through
-      // the lo face's region [lo - delta, inner_lo] and leaves through the hi
-      // face's [inner_hi, hi + delta]; NaN bounds (0 * inf on a plane) are
-      // dropped by fmaxf / fminf: no constraint, the conservative side
-      const bool pos = (fbits(nd) >> 31) == 0u;
-      neg |= pos ? 0u : 1u << a;
-      e0[a] = pos ? tl : th;
-      e1[a] = pos ? til : tih;
-      x0[a] = pos ? tih : til;
-      x1[a] = pos ? th : tl;
-      T0 = fmaxf(T0, e0[a]);
-      T1 = fminf(T1, x1[a]);
-    }
-    const bool box = (T0 <= T1) & (own_skip != c);
-    // candidate faces (bit 2a + side, side 1 = the hi face): the ray inside
-    // the face's region while inside the padded box; the first is the one
-    // whose region starts first (the face the ray enters through)
-    uint32_t cand = 0u, first = 8u;
-    float first_t = __builtin_inff();
-#pragma unroll
-    for (uint32_t a = 0; a < 3; ++a) {
-      const float es = fmaxf(e0[a], T0), xs = fmaxf(x0[a], T0);
-      const bool ce = box & (es <= fminf(e1[a], T1));
-      const bool cl = box & (xs <= fminf(x1[a], T1));
-      const uint32_t ebit = 2u * a + ((neg >> a) & 1u), lbit = ebit ^ 1u;
-      cand |= (ce ? 1u << ebit : 0u) | (cl ? 1u << lbit : 0u);
-      if (ce & (es < first_t)) { first_t = es; first = ebit; }
-      if (cl & (xs < first_t)) { first_t = xs; first = lbit; }
-    }
-    if (first < 8u) {
-      uint32_t pr = 0xFFFFFFFFu;
-#pragma unroll
-      for (uint32_t k = 0; k < 6; ++k) pr = first == k ? sc.conv_near_tris[c][k] : pr;
-      pair_nearest<MODE>(sc, cx, o, d, pr, h);
-      cand &= ~(1u << first);
-    }
-    // the other candidates, each while its region starts before h.t (1 + 2^-11)
-#pragma unroll
-    for (uint32_t a = 0; a < 3; ++a) {
-      const uint32_t ebit = 2u * a + ((neg >> a) & 1u), lbit = ebit ^ 1u;
-      if (((cand >> ebit) & 1u) && fmaxf(e0[a], T0) <= h.t * kCullScale) {
-        uint32_t pr = 0xFFFFFFFFu;
-#pragma unroll
-        for (uint32_t k = 0; k < 6; ++k) pr = ebit == k ? sc.conv_near_tris[c][k] : pr;
-        pair_nearest<MODE>(sc, cx, o, d, pr, h);
-      }
-      if (((cand >> lbit) & 1u) && fmaxf(x0[a], T0) <= h.t * kCullScale) {
-        uint32_t pr = 0xFFFFFFFFu;
-#pragma unroll
-        for (uint32_t k = 0; k < 6; ++k) pr = lbit == k ? sc.conv_near_tris[c][k] : pr;
-        pair_nearest<MODE>(sc, cx, o, d, pr, h);
-      }
-    }
-  }
-  // -- walls
-  {
-    float te = h.t * kCullScale;
-    uint32_t wmask = 0u;
-    float tlo[kMaxOccPlanes];
-#pragma unroll
-    for (uint32_t k = 0; k < kMaxOccPlanes; ++k) {
-      tlo[k] = __builtin_inff();
-      if (k < sc.occ_planes) {   // wave-uniform
-        const float* p = sc.occ_plane[k];
-        const float nd = (p[0] * d.x + p[1] * d.y) + p[2] * d.z;
-        const float dist = p[3] - ((p[0] * o.x + p[1] * o.y) + p[2] * o.z);   // > 0 inside
-        if (nd > 0.0f) {   // approached
-          const float inv = m_rcp(nd);
-          tlo[k] = (dist - sc.room_delta) * inv;
-          te = fminf(te, (dist + sc.room_delta) * inv);
-          wmask |= (nd < sc.room_graze ? 1u : 0u) << k;   // grazing: always a candidate
-        }
-      }
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kMaxOccPlanes; ++k)   // (tlo is +inf for planes not approached)
-      if (k < sc.occ_planes) wmask |= (tlo[k] < __builtin_inff() && tlo[k] <= te) ? 1u << k : 0u;
-    while (wmask) {   // per lane: its candidate walls, lowest plane first
-      const uint32_t k = __builtin_ctz(wmask);
-      wmask &= wmask - 1u;
-      uint32_t p0 = 0xFFFFFFFFu, p1 = 0xFFFFFFFFu;
-#pragma unroll
-      for (uint32_t j = 0; j < kMaxOccPlanes; ++j) {
-        p0 = k == j ? sc.wall_pairs[j][0] : p0;
-        p1 = k == j ? sc.wall_pairs[j][1] : p1;
-      }
-      pair_nearest<MODE>(sc, cx, o, d, p0, h);
-      if (p1 != 0xFFFFFFFFu) pair_nearest<MODE>(sc, cx, o, d, p1, h);
-    }
-  }
-  // -- lights (the light record's vertices are the primitive's, in its order)
-  for (uint32_t k = 0; k < sc.num_lights; ++k) {   // wave-uniform
-    const float4 LB = fetch_light<MODE>(sc, cx, k, 1), LD = fetch_light<MODE>(sc, cx, k, 3);
-    const float4 LF = fetch_light<MODE>(sc, cx, k, 5);
-    const uint32_t prim = fbits(LD.w);
-    const V3 p0 = mk(LB);
-    float t, u, v;
-    const bool ok = tri_bary(o, d, p0, sub(mk(LD), p0), sub(mk(LF), p0), t, u, v);
-    const bool hit = ok & (t >= 0.0f) & (t <= h.t);
-    if (hit & (!h.found | (t < h.t) | (prim < h.prim))) {
-      h.found = true;
-      h.t = t;
-      h.u = u;
-      h.v = v;
-      h.prim = prim;
-    }
-  }
 }
 
 template <int STACK, int MODE>
@@ -1695,7 +1498,6 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
   // -- phase 0: generate (bounce 0) or load (SoA queue planes 0-1) the ray
   PathState s;
   uint32_t tag = 0;   // tag = global owned slot | prevDiffuse << 31
-  uint32_t origin = 0xFFFFFFFFu;   // the primitive the ray leaves (queue plane 1 .w; camera rays: none)
   uint32_t pblk = 0xFFFFFFFFu;   // bounce 0: the pixel's 8x8 block (camera-ray candidate lists)
   if (active) {
     if (bounce == 0) {
@@ -1719,7 +1521,6 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
       s.o = mk(q0);
       tag = fbits(q0.w);
       s.d = mk(q1);
-      origin = fbits(q1.w);
       s.prevDiffuse = (tag >> 31) ? 1.0f : 0.0f;
     }
   }
@@ -1756,8 +1557,6 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
         const int32_t root = shadow_root(sc, s.o, graze);
         if (!(a.debug & 64u) && traverse<STACK, MODE, true>(sc, cx, s.o, s.d, 0.0f, hh, h.prim, root)) h.found = false;
       }
-    } else if (sc.room_nearest && !(a.debug & 2048u) && inside_room(sc, s.o)) {
-      room_nearest<MODE>(sc, cx, s.o, s.d, origin, h);   // no walk: walls, solids' faces, lights
     } else {
       h = trace_nearest<STACK, MODE>(sc, cx, s.o, s.d, 0.0f, __builtin_inff());
     }
@@ -1828,7 +1627,7 @@ __device__ __forceinline__ uint32_t bounce_wave(const DeviceScene& sc, const Lds
     o = cls1 ? out_base + cap - 1u - (w1 + lanes_below_in(mask1)) : out_base + w0 + lanes_below_in(mask0);
     if (alive && !(a.debug & 4u)) {
       out_q.plane[0][o] = make_float4(s.o.x, s.o.y, s.o.z, bitsf(gslot | (s.prevDiffuse != 0.0f ? 0x80000000u : 0u)));
-      out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, bitsf(h.prim));
+      out_q.plane[1][o] = make_float4(s.d.x, s.d.y, s.d.z, 0.0f);
       out_q.plane[2][o] = make_float4(s.T.x, s.T.y, s.T.z, s.pdf);
     }
     wrote = (uint32_t)__popcll(mask0 | mask1);

@@ -136,15 +136,6 @@ struct DeviceScene {
   uint32_t conv_count;
   float conv_obb[4][16];             // [kMaxConvex]
   uint32_t conv_face_tris[4][8];
-  // nearest queries from inside the room (kernels.hip room_nearest,
-  // mrt_scene_info ABI 10): per solid each face's reach along its axis and
-  // its triangles with the culled bottoms; per culled plane its triangles
-  uint32_t room_nearest;
-  float room_graze;
-  float room_delta;                  // the walls' crossing padding (= the solids' delta)
-  float conv_inner[4][6];
-  uint32_t conv_near_tris[4][6];
-  uint32_t wall_pairs[8][2];
 };
 constexpr uint32_t kMaxOccPlanes = 8;
 // convex occluders (DeviceScene::conv_*): at most this many solids, and the
@@ -152,10 +143,6 @@ constexpr uint32_t kMaxOccPlanes = 8;
 // the ray to skip that face's solid (kernels.hip convex_occlusion)
 constexpr uint32_t kMaxConvex = 4;
 constexpr float kConvexLeaveDot = 1e-3f;
-// room_nearest: a culled plane the ray approaches at |cos| below this has its
-// triangles tested whatever its padded crossing (the leaf test's error grows
-// as 1 / |cos|)
-constexpr float kRoomGraze = 0.02f;
 // the origin-triangle early-out pays where a shadow ray's descent to its own
 // leaf goes through global memory: measured C4 (1M triangles) +2.6 %, C3
 // (7 K) +0.5 % (with the path kernel's inline shadow finishes), C2 (36, the

@@ -154,7 +154,6 @@ bool find_occluders(const float* positions, size_t stride_bytes, uint32_t num_ve
   for (const Plane& P : used) {
     for (uint32_t t : P.tris) culled[t] = 1;
     out.planes.push_back({(float)P.n.x, (float)P.n.y, (float)P.n.z, (float)P.w});
-    out.plane_tris.push_back(P.tris);
   }
   for (uint32_t t = 0; t < num_triangles; ++t) {
     if (culled[t]) ++out.culled;
@@ -264,7 +263,7 @@ bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t 
           cen = {cen.x + v.x, cen.y + v.y, cen.z + v.z};
         }
     cen = {cen.x / pts.size(), cen.y / pts.size(), cen.z / pts.size()};
-    struct Face { D3 n; double w; std::vector<uint32_t> tris; std::vector<uint32_t> culled; };
+    struct Face { D3 n; double w; std::vector<uint32_t> tris; };
     std::vector<Face> faces;
     for (size_t i : slots) {
       const uint32_t t = keep[i];
@@ -285,33 +284,19 @@ bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t 
       Face* on = nullptr;
       for (Face& F : faces)
         if (dot(F.n, n) > 1.0 - 1e-9 && std::fabs(F.w - w) <= tol) { on = &F; break; }
-      if (!on) { faces.push_back(Face{n, w, {}, {}}); on = &faces.back(); }
+      if (!on) { faces.push_back(Face{n, w, {}}); on = &faces.back(); }
       on->tris.push_back(t);
       if (on->tris.size() > 2) return false;
     }
     // the culled planes the solid stands on (its missing faces, e.g. a box's bottom)
-    for (size_t k = 0; k < occ.planes.size(); ++k) {
-      const auto& cp = occ.planes[k];
+    for (const auto& cp : occ.planes) {
       const D3 n{cp[0], cp[1], cp[2]};
       const double w = cp[3];
       bool touches = false;
       for (const D3& v : pts) touches |= std::fabs(dot(n, v) - w) <= tol;
       bool dup = false;
       for (const Face& F : faces) dup |= dot(F.n, n) > 1.0 - 1e-9 && std::fabs(F.w - w) <= tol;
-      if (touches && !dup) {
-        // the plane's triangles with every corner a corner of this solid (the
-        // block's bottom): culled for shadow rays, but part of the solid for
-        // nearest queries (room_nearest)
-        Face F{n, w, {}, {}};
-        if (k < occ.plane_tris.size())
-          for (uint32_t t : occ.plane_tris[k]) {
-            bool mine = true;
-            for (int c = 0; c < 3 && mine; ++c) mine = pos_id.count(key(indices[3 * t + c])) != 0;
-            for (int c = 0; c < 3 && mine; ++c) mine = seen[pos_id[key(indices[3 * t + c])]] != 0;
-            if (mine) F.culled.push_back(t);
-          }
-        faces.push_back(std::move(F));
-      }
+      if (touches && !dup) faces.push_back(Face{n, w, {}});
     }
     // convex: every corner inside every face plane
     for (const Face& F : faces)
@@ -324,23 +309,11 @@ bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t 
     std::array<uint32_t, 8> ft;
     ft.fill(0xFFFFFFFFu);
     std::array<float, 18> fn{};
-    std::array<float, 6> inner{};
-    std::array<uint32_t, 6> near{};
-    near.fill(0xFFFFFFFFu);
     std::vector<uint8_t> used(6, 0);
     uint32_t axis = 0;
     auto pack = [&](const Face& F) -> uint32_t {
       const uint32_t t0 = F.tris.size() > 0 ? F.tris[0] : 0xFFFFu, t1 = F.tris.size() > 1 ? F.tris[1] : 0xFFFFu;
       return (t0 & 0xFFFFu) | (t1 << 16);
-    };
-    // nearest queries: the face's triangles, a culled face's (the bottom) included
-    bool near_ok = true;
-    auto pack_near = [&](const Face& F) -> uint32_t {
-      const std::vector<uint32_t>& ts = F.tris.empty() ? F.culled : F.tris;
-      if (ts.size() > 2) near_ok = false;
-      for (uint32_t t : ts) near_ok = near_ok && t < 0xFFFFu;
-      const uint32_t t0 = ts.size() > 0 ? ts[0] : 0xFFFFu, t1 = ts.size() > 1 ? ts[1] : 0xFFFFu;
-      return (t0 & 0xFFFFu) | ((t1 & 0xFFFFu) << 16);
     };
     for (size_t i = 0; i < 6 && axis < 3; ++i) {
       if (used[i]) continue;
@@ -364,21 +337,6 @@ bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t 
       for (const D3& v : pts) { lo = std::min(lo, dot(na, v)); hi = std::max(hi, dot(na, v)); }
       obb[9 + 2 * axis] = std::nextafter((float)(lo - delta), -INFINITY);
       obb[9 + 2 * axis + 1] = std::nextafter((float)(hi + delta), INFINITY);
-      // each face's own extent along n (the faces of a skewed solid are not
-      // quite perpendicular to it): the lo face's corners reach up to
-      // inner[2a] - delta, the hi face's down to inner[2a + 1] + delta
-      double lo_face_max = -1e300, hi_face_min = 1e300;
-      for (const D3& v : pts) {
-        if (std::fabs(dot(L.n, v) - L.w) <= tol) lo_face_max = std::max(lo_face_max, dot(na, v));
-        if (std::fabs(dot(H.n, v) - H.w) <= tol) hi_face_min = std::min(hi_face_min, dot(na, v));
-      }
-      if (!(lo_face_max > -1e300) || !(hi_face_min < 1e300)) return false;
-      inner[2 * axis] = std::nextafter((float)(lo_face_max + delta), INFINITY);
-      inner[2 * axis + 1] = std::nextafter((float)(hi_face_min - delta), -INFINITY);
-      near[2 * axis] = pack_near(L);
-      near[2 * axis + 1] = pack_near(H);
-      for (uint32_t t : (L.tris.empty() ? L.culled : L.tris)) out.near_claimed.push_back(t);
-      for (uint32_t t : (H.tris.empty() ? H.culled : H.tris)) out.near_claimed.push_back(t);
       for (uint32_t t : L.tris) { if (t >= 0xFFFFu) return false; out.prim_face[t] = out.count * 8 + 2 * axis + 1; }
       for (uint32_t t : H.tris) { if (t >= 0xFFFFu) return false; out.prim_face[t] = out.count * 8 + 2 * axis + 2; }
       ft[2 * axis] = pack(L);
@@ -394,9 +352,6 @@ bool find_convex_occluders(const float* vertices, size_t stride_bytes, uint32_t 
     out.obb.push_back(obb);
     out.face_tris.push_back(ft);
     out.face_normal.push_back(fn);
-    out.inner.push_back(inner);
-    out.near_tris.push_back(near);
-    out.near_ok = out.near_ok && near_ok;
     out.count += 1;
   }
   out.delta = (float)delta;

@@ -32,7 +32,6 @@ struct OccluderSet {
   float cos_min = 0.0f;                        // shadow rays with |cos| to the light's normal below this
                                                //   traverse the main tree (grazing guard, occluders.cpp)
   uint32_t culled = 0;                         // triangles left out
-  std::vector<std::vector<uint32_t>> plane_tris;   // per entry of `planes`: the triangles on it (ascending)
 };
 
 // positions: 3 floats per vertex at `stride_bytes`; light_vertices and
@@ -74,13 +73,6 @@ struct ConvexSet {
   std::vector<std::array<float, 16>> obb;          // per solid, see above
   std::vector<std::array<uint32_t, 8>> face_tris;  // per solid: 6 faces (+2 unused, 0xFFFFFFFF)
   std::vector<std::array<float, 18>> face_normal;  // per solid: face k's outward unit normal at [3k, 3k+3)
-  // nearest queries from inside the room (kernels.hip room_nearest):
-  std::vector<std::array<float, 6>> inner;         // per solid: [2a] = the lo face's reach along axis a
-                                                   //   (+ delta), [2a + 1] = the hi face's (- delta)
-  std::vector<std::array<uint32_t, 6>> near_tris;  // per solid: face_tris with the culled faces' own
-                                                   //   triangles (the bottoms) filled in
-  std::vector<uint32_t> near_claimed;              // every primitive on a solid (bottoms included)
-  bool near_ok = true;                             // every face has <= 2 triangles with 16-bit ids
   std::vector<uint32_t> prim_face;                 // per scene primitive, see above
   float delta = 0.0f;
 };

@@ -989,37 +989,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
       for (int i = 0; i < 16; ++i) in.convex_obb[c][i] = conv.obb[c][i];
       for (int k = 0; k < 8; ++k) in.convex_face_tris[c][k] = conv.face_tris[c][k];
     }
-    // nearest queries from inside the room (kernels.hip room_nearest): every
-    // triangle a light, a wall triangle of one culled plane (<= 4 per plane)
-    // or a solid's (bottoms included), exactly once, ids below 0xFFFF
-    bool room = conv.near_ok && T < 0xFFFFu && occ.plane_tris.size() == occ.planes.size() &&
-                h.light_count <= mrt::kLightShortcutMax;
-    if (const char* v = mrt::diag_env("MRT_ROOM")) room = room && std::atoi(v) != 0;
-    std::vector<uint8_t> cls(T, 0);
-    for (uint32_t l = 0; l < h.light_count && room; ++l) room = h.lights[l].index < T && !cls[h.lights[l].index]++;
-    for (uint32_t t : conv.near_claimed) room = room && t < T && !cls[t]++;
-    for (size_t k = 0; k < occ.plane_tris.size() && room; ++k) {
-      std::vector<uint32_t> wall;
-      for (uint32_t t : occ.plane_tris[k])
-        if (!cls[t]) { wall.push_back(t); cls[t] = 1; }
-      room = room && wall.size() <= 4;
-      for (int j = 0; j < 2 && room; ++j) {
-        const uint32_t a = 2u * j < wall.size() ? wall[2 * j] : 0xFFFFu, b = 2u * j + 1 < wall.size() ? wall[2 * j + 1] : 0xFFFFu;
-        in.wall_pairs[k][j] = (a & 0xFFFFu) | (b << 16);
-      }
-    }
-    for (uint32_t t = 0; t < T && room; ++t) room = cls[t] == 1;
-    if (room) {
-      in.room_nearest = 1;
-      in.room_graze = mrt::kRoomGraze;
-      for (uint32_t c = 0; c < conv.count; ++c)
-        for (int k = 0; k < 6; ++k) {
-          in.convex_inner[c][k] = conv.inner[c][k];
-          in.convex_near_tris[c][k] = conv.near_tris[c][k];
-        }
-    } else {
-      std::memset(in.wall_pairs, 0, sizeof(in.wall_pairs));
-    }
   }
   if (occ_on) {
     in.occluder_planes = (uint32_t)occ.planes.size();
@@ -1099,12 +1068,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   d.conv_count = in.convex_solids;
   std::memcpy(d.conv_obb, in.convex_obb, sizeof(d.conv_obb));
   std::memcpy(d.conv_face_tris, in.convex_face_tris, sizeof(d.conv_face_tris));
-  d.room_nearest = in.room_nearest;
-  d.room_graze = in.room_graze;
-  d.room_delta = in.convex_delta;
-  std::memcpy(d.conv_inner, in.convex_inner, sizeof(d.conv_inner));
-  std::memcpy(d.conv_near_tris, in.convex_near_tris, sizeof(d.conv_near_tris));
-  std::memcpy(d.wall_pairs, in.wall_pairs, sizeof(d.wall_pairs));
   HIP_TRY(alloc_isect_spill(s->isect_spill, d.max_stack));
   in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
   *out = s.release();

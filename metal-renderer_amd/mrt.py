@@ -103,9 +103,6 @@ class SceneInfo(ctypes.Structure):
         ("occluder_plane", (ctypes.c_float * 4) * 8),
         ("convex_solids", ctypes.c_uint32), ("convex_delta", ctypes.c_float),
         ("convex_obb", (ctypes.c_float * 16) * 4), ("convex_face_tris", (ctypes.c_uint32 * 8) * 4),
-        ("room_nearest", ctypes.c_uint32), ("room_graze", ctypes.c_float),
-        ("convex_inner", (ctypes.c_float * 6) * 4), ("convex_near_tris", (ctypes.c_uint32 * 6) * 4),
-        ("wall_pairs", (ctypes.c_uint32 * 2) * 8),
     ]
 
 

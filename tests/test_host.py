@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(mrt_mod):
     missing = [n for n in sorted(declared) if not hasattr(lib, n)]
     assert not missing, missing
     assert set(mrt_mod.EXPORTED) == declared
-    assert mrt_mod.lib().mrt_abi_version() == 10
+    assert mrt_mod.lib().mrt_abi_version() == 9
 
 
 def test_objc_facade_binds_only_declared_symbols(mrt_mod):
