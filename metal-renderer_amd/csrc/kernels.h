@@ -112,8 +112,7 @@ struct BounceArgs {
                                //   128 = no origin-triangle test (stream / bounce kernels),
                                //   256 = the accumulate touches no pixel (renderer.cpp draw_n),
                                //   512 = no convex-occluder test, 1024 = no other-light test (occluder-tree
-                               //   shadow queries, stream / bounce kernels), 4096 = convex occluders without
-                               //   face tests (a segment through a padded solid counts as occluded)
+                               //   shadow queries, stream / bounce kernels)
   // segmented queues: block g of a launch appends its class-0 survivors
   // (left a diffuse surface) to [g*cap, g*cap + c0_g) and its class-1
   // survivors to [g*cap + cap - c1_g, g*cap + cap) of the output queue

@@ -855,7 +855,7 @@ __device__ __forceinline__ bool face_occludes(const DeviceScene& sc, const LdsCt
 // Returns whether a solid occludes; the occluder tree is not walked.
 template <int MODE>
 __device__ __forceinline__ bool convex_occlusion(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, uint32_t target,
-                                                 float tT, uint32_t origin, uint32_t dbg = 0u) {
+                                                 float tT, uint32_t origin) {
   const uint32_t own = fbits(fetch_prim<MODE>(sc, cx, origin, 2).w);   // c * 8 + face + 1 of the origin's solid
   const V3 own_n = mk(fetch_prim<MODE>(sc, cx, origin, 3).w, fetch_prim<MODE>(sc, cx, origin, 4).w,
                       fetch_prim<MODE>(sc, cx, origin, 5).w);   // its face's outward unit normal (0 off the solids)
@@ -884,7 +884,6 @@ __device__ __forceinline__ bool convex_occlusion(const DeviceScene& sc, const Ld
       fout = out_ ? (pos ? 2u * a + 1u : 2u * a) : fout;
     }
     const bool leaves_own = own_skip == c;
-    if ((dbg & 4096u) && (t0 <= t1) & !leaves_own) occluded = true;   // ablation: no face tests
     if ((t0 <= t1) & !leaves_own & !occluded) {
       uint32_t pin = 0xFFFFFFFFu, pout = 0xFFFFFFFFu;
 #pragma unroll
@@ -918,7 +917,7 @@ __device__ __forceinline__ bool trace_occluded(const DeviceScene& sc, const LdsC
   int32_t root = shadow_root(sc, o, graze);
   const bool via_occ = root == sc.occ_root;
   if (sc.conv_count && via_occ) {
-    if (!(dbg & 512u) && convex_occlusion<MODE>(sc, cx, o, d, target, t_target, origin, dbg)) return true;
+    if (!(dbg & 512u) && convex_occlusion<MODE>(sc, cx, o, d, target, t_target, origin)) return true;
     root = kDone;   // no walk (the light triangles are still tested below)
   }
   if (sc.occ_lights && via_occ && !(dbg & 1024u) && lights_occlude<MODE>(sc, cx, o, d, target, tl, t_target)) return true;
