@@ -1803,11 +1803,13 @@ __global__ __launch_bounds__(kBlock, MRT_BOUNCE_WAVES) void bounce_kernel(Device
 // No wave ever waits for another, so any grid and any residency is safe.
 // ---------------------------------------------------------------------------
 template <int STACK, int MODE>
-// Waves per SIMD the stream kernel's registers allow: 6 (80 VGPRs, 9 values
-// spilled to scratch) under the max-ILP scheduler of its unit (Makefile):
+// Waves per SIMD the stream kernel's registers allow: 6 (80 VGPRs, 6 values
+// spilled to scratch, reloaded outside the traversal loops: tools/
+// scratch_sites.py) under the max-ILP scheduler of its unit (Makefile):
 // C2 +1.7…+3.4 %, L = 5 +4…6 % over 5 waves (96 VGPRs, no spill); 7 / 8
 // waves (23 / 37 spills) lose 6 / 27 %, and 6 waves under the default
-// scheduler only tie (r5, alternating in one call)
+// scheduler only tie (r5, alternating in one call); re-swept at the r6
+// library: 5 / 7 waves -6 / -10 %, 0 / 2 spare block slots -2 / -1.3 %
 #ifndef MRT_STREAM_WAVES
 #define MRT_STREAM_WAVES 6
 #endif
