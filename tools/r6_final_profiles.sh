@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 T=${TAG:-r6a}
 bash tools/profile.sh $T c2 || exit $?
-LPS=64 STEPS=6 bash tools/profile.sh $T c2i || exit $?
+LPS=64 STEPS=6 bash tools/profile.sh $T c2i --no-image-check || exit $?   # (the image check's 64-frame launches would join the per-frame ones)
 bash tools/profile.sh $T c2l5 || exit $?
 NAME=c2s8 STEPS=40 WARM=4 bash tools/profile.sh $T c2 --shard-of 8 || exit $?
 STEPS=6 WARM=1 bash tools/profile.sh $T c3 || exit $?
