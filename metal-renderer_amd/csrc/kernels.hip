@@ -562,61 +562,12 @@ __device__ __forceinline__ int32_t stack_pop(const LdsCtx& cx, int& sp) {
 // such cases (it never changes an answer: the leaf tests' t <= h.t rule
 // decides).
 [[maybe_unused]] constexpr float kCullScale = 1.0f + 0x1p-11f;
-// Quantised global nodes (MRT_QNODES builds; renderer.cpp quantize_nodes):
-// the box test of a 64-B node whose child planes are o + q s (8-bit q),
-// straight from the bytes: t(q) = q (s inv) + (o - origin) inv per axis,
-// the near / far byte words chosen by the direction's signs (the rows in ray
-// order, as fetch_node4's).  Every decoded box holds its child's padded box,
-// so the traversal's answers are the fp32 nodes'.
-#ifndef MRT_QNODES
-#define MRT_QNODES 0
-#endif
-__device__ __forceinline__ float qslab(uint32_t word, int k, float a, float b) {
-  const float q = (float)((word >> (8 * k)) & 255u);
-#if MRT_PRECISE
-  return q * a + b;
-#else
-  return fmaf(q, a, b);
-#endif
-}
-__device__ __forceinline__ void qnode_box4(const DeviceScene& sc, int32_t node, V3 o, const RayBox& rb, float tmin,
-                                           float tmax, float tn[4], int32_t r[4]) {
-  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(sc.qnodes);
-  const uint32_t b = (uint32_t)node << 6;
-  const float4 f0 = buf_ld4(rs, b), f1 = buf_ld4(rs, b + 16u), f2 = buf_ld4(rs, b + 32u), f3 = buf_ld4(rs, b + 48u);
-#if MRT_PRECISE
-  const float bx = (f0.x - o.x) * rb.inv.x, by = (f0.y - o.y) * rb.inv.y, bz = (f0.z - o.z) * rb.inv.z;
-#else
-  const float bx = fmaf(f0.x, rb.inv.x, -rb.oinv.x), by = fmaf(f0.y, rb.inv.y, -rb.oinv.y);
-  const float bz = fmaf(f0.z, rb.inv.z, -rb.oinv.z);
-  (void)o;
-#endif
-  const float ax = f0.w * rb.inv.x, ay = f1.x * rb.inv.y, az = f1.y * rb.inv.z;
-  const bool nx = (fbits(rb.inv.x) >> 31) != 0u, ny = (fbits(rb.inv.y) >> 31) != 0u, nz = (fbits(rb.inv.z) >> 31) != 0u;
-  const uint32_t xl = fbits(f1.z), xh = fbits(f1.w), yl = fbits(f2.x), yh = fbits(f2.y), zl = fbits(f2.z),
-                 zh = fbits(f2.w);
-  const uint32_t xn = nx ? xh : xl, xf = nx ? xl : xh, yn = ny ? yh : yl, yf = ny ? yl : yh, zn = nz ? zh : zl,
-                 zf = nz ? zl : zh;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float tnear = fmaxf(fmaxf(qslab(xn, k, ax, bx), qslab(yn, k, ay, by)), fmaxf(qslab(zn, k, az, bz), tmin));
-    const float tfar = fminf(fminf(qslab(xf, k, ax, bx), qslab(yf, k, ay, by)), fminf(qslab(zf, k, az, bz), tmax));
-    tn[k] = tnear <= tfar ? tnear : __builtin_inff();
-  }
-  r[0] = (int32_t)fbits(f3.x); r[1] = (int32_t)fbits(f3.y); r[2] = (int32_t)fbits(f3.z); r[3] = (int32_t)fbits(f3.w);
-}
-
 template <int STACK, int MODE, bool ANY>
 __device__ __forceinline__ int32_t interior_step(const DeviceScene& sc, const LdsCtx& cx, int32_t node, V3 o,
                                                  const RayBox& rb, float tmin, float tmax, int& sp) {
   {
     float t[4];
     int32_t r[4];
-#if MRT_QNODES
-    if (MODE == kTopLds && (uint32_t)node >= cx.n_lds_nodes && sc.qnodes) {
-      qnode_box4(sc, node, o, rb, tmin, tmax * kCullScale, t, r);
-    } else
-#endif
     {
       float4 q[7];
       fetch_node4<MODE>(sc, cx, node, rb, q);

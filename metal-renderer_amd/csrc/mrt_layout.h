@@ -85,8 +85,6 @@ constexpr uint32_t kIntersectSpillGrid = 1024;      // persistent grid of the st
 // 4 floats per record.
 struct DeviceScene {
   const float* nodes;        // float4 x 8 per BVH4 node (see above)
-  const float* qnodes;       // float4 x 4 per node, 8-bit quantised boxes (renderer.cpp quantize_nodes),
-                             //   read for global nodes by MRT_QNODES builds; null: none
   const float* tris;         // float4 x 3 per leaf-ordered triangle: (v0, bits(prim)), (e1, 0), (e2, 0)
   const float* prims;        // float4 x 6 per primitive (original order):
                              //   (p0, bits(material)), (p1, bits(light index or ~0u)), (p2, 0),

@@ -111,7 +111,7 @@ struct mrt_scene {
   std::vector<uint32_t> occ_keep;   // primitives the occluder tree holds
   int32_t occ_root = 0;
   uint32_t occ_node_base = 0, occ_max_stack = 0;
-  DevBuf nodes, qnodes, tris, prims, materials, lights;
+  DevBuf nodes, tris, prims, materials, lights;
   mrt::DeviceScene dev{};
   mrt_scene_info info{};
 };
@@ -764,60 +764,6 @@ int mrt_noise_table(uint64_t seed, int64_t frame, float* out) {
 // ---------------------------------------------------------------------------
 // scene
 // ---------------------------------------------------------------------------
-// 8-bit quantised BVH4 nodes (64 B instead of 128 B; read by MRT_QNODES
-// builds for the nodes below the LDS-staged top).  Node i = 16 words:
-//   [0..2] origin o (the live children's box lo, floats), [3] scale s.x,
-//   [4] s.y, [5] s.z, [6] / [7] = x lo / hi bytes of children 0..3 (byte k =
-//   child k), [8] / [9] y lo / hi, [10] / [11] z lo / hi, [12..15] refs.
-// A child's plane decodes to o + q s: lo bytes rounded down and hi bytes up
-// (checked in double against the float box), so every decoded box holds
-// its child's box (which is padded already, bvh.cpp) — the traversal's
-// answers are unchanged, it only enters a few more boxes.  Empty slots get
-// q_lo = 255, q_hi = 0: an inverted box on every axis (s > 0 always).
-static std::vector<uint32_t> quantize_nodes(const std::vector<float>& nodes) {
-  const size_t n = nodes.size() / 32;
-  std::vector<uint32_t> q(16 * n, 0u);
-  for (size_t i = 0; i < n; ++i) {
-    const float* f = &nodes[32 * i];
-    uint32_t* o = &q[16 * i];
-    bool live[4];
-    for (int k = 0; k < 4; ++k) live[k] = (int32_t)fbits(f[24 + k]) != mrt::kEmptyChild;
-    for (int a = 0; a < 3; ++a) {
-      float lo = INFINITY, hi = -INFINITY;
-      for (int k = 0; k < 4; ++k)
-        if (live[k]) { lo = std::min(lo, f[8 * a + k]); hi = std::max(hi, f[8 * a + 4 + k]); }
-      if (!(lo <= hi)) { lo = 0.0f; hi = 0.0f; }   // no live child
-      // s > 0 and 255 s >= hi - lo in double (a floor of 2^-20 (|lo| + 1) keeps
-      // empty slots inverted on a flat axis)
-      float sc = (float)(((double)hi - (double)lo) / 255.0);
-      sc = std::max(sc, (float)((std::fabs((double)lo) + 1.0) * 0x1p-20));
-      while ((double)lo + 255.0 * (double)sc < (double)hi) sc = std::nextafter(sc, INFINITY);
-      uint32_t wlo = 0, whi = 0;
-      for (int k = 0; k < 4; ++k) {
-        uint32_t ql = 255u, qh = 0u;
-        if (live[k]) {
-          const double cl = f[8 * a + k], ch = f[8 * a + 4 + k];
-          double dl = std::floor((cl - lo) / sc), dh = std::ceil((ch - lo) / sc);
-          dl = std::min(255.0, std::max(0.0, dl));
-          dh = std::min(255.0, std::max(0.0, dh));
-          while (dl > 0.0 && (double)lo + dl * (double)sc > cl) dl -= 1.0;
-          while (dh < 255.0 && (double)lo + dh * (double)sc < ch) dh += 1.0;
-          ql = (uint32_t)dl;
-          qh = (uint32_t)dh;
-        }
-        wlo |= ql << (8 * k);
-        whi |= qh << (8 * k);
-      }
-      o[a] = fbits(lo);
-      o[3 + a] = fbits(sc);
-      o[6 + 2 * a] = wlo;
-      o[7 + 2 * a] = whi;
-    }
-    for (int k = 0; k < 4; ++k) o[12 + k] = fbits(f[24 + k]);
-  }
-  return q;
-}
-
 int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (!desc || !out || !desc->obj_path) return fail(MRT_ERR_INVALID, "mrt_scene_create: null argument");
   *out = nullptr;
@@ -1080,18 +1026,12 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (builder == MRT_BVH_HOST_SAH) {
     HIP_TRY(upload(s->nodes, up_nodes.data(), up_nodes.size() * 4));
     HIP_TRY(upload(s->tris, up_tris.data(), up_tris.size() * 4));
-    // quantised copies of the nodes for scenes traversed from global memory
-    if (T >= 65536) {
-      const std::vector<uint32_t> qn = quantize_nodes(up_nodes);
-      HIP_TRY(upload(s->qnodes, qn.data(), qn.size() * 4));
-    }
   }
   HIP_TRY(upload(s->prims, prims.data(), prims.size() * 4));
   HIP_TRY(upload(s->materials, mats.data(), mats.size() * 4));
   HIP_TRY(upload(s->lights, lights.data(), lights.size() * 4));
   mrt::DeviceScene& d = s->dev;
   d.nodes = s->nodes.as<float>();
-  d.qnodes = s->qnodes.bytes ? s->qnodes.as<float>() : nullptr;
   d.tris = s->tris.as<float>();
   d.prims = s->prims.as<float>();
   d.materials = s->materials.as<float>();
@@ -1129,7 +1069,7 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   std::memcpy(d.conv_obb, in.convex_obb, sizeof(d.conv_obb));
   std::memcpy(d.conv_face_tris, in.convex_face_tris, sizeof(d.conv_face_tris));
   HIP_TRY(alloc_isect_spill(s->isect_spill, d.max_stack));
-  in.device_bytes = s->nodes.bytes + s->qnodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
+  in.device_bytes = s->nodes.bytes + s->tris.bytes + s->prims.bytes + s->materials.bytes + s->lights.bytes;
   *out = s.release();
   return MRT_OK;
 }
