@@ -153,24 +153,6 @@ __device__ __forceinline__ bool tri_bary(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float&
   return (det != 0.0f) & (b1 >= 0.0f) & (b1 <= 1.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f);
 }
 
-// Unit-triangle (Woop) test of an MRT_WOOP build's leaf record (A/B): the
-// ray in the triangle's own frame, t from the plane row, (b1, b2) from the
-// others; (u, v) as tri_bary's.
-__device__ __forceinline__ bool tri_woop(V3 o, V3 d, const float4& r0, const float4& r1, const float4& r2, float& t,
-                                         float& u, float& v) {
-  const float oz = fmaf(r2.x, o.x, fmaf(r2.y, o.y, fmaf(r2.z, o.z, r2.w)));
-  const float dz = fmaf(r2.x, d.x, fmaf(r2.y, d.y, r2.z * d.z));
-  t = -oz * m_rcp(dz);
-  const float ox = fmaf(r0.x, o.x, fmaf(r0.y, o.y, fmaf(r0.z, o.z, r0.w)));
-  const float dx = fmaf(r0.x, d.x, fmaf(r0.y, d.y, r0.z * d.z));
-  const float oy = fmaf(r1.x, o.x, fmaf(r1.y, o.y, fmaf(r1.z, o.z, r1.w)));
-  const float dy = fmaf(r1.x, d.x, fmaf(r1.y, d.y, r1.z * d.z));
-  const float b1 = fmaf(t, dx, ox), b2 = fmaf(t, dy, oy);
-  u = (1.0f - b1) - b2;
-  v = b1;
-  return (dz != 0.0f) & (b1 >= 0.0f) & (b2 >= 0.0f) & (b1 + b2 <= 1.0f);
-}
-
 struct Hit {
   float t, u, v;
   uint32_t prim;
@@ -311,12 +293,6 @@ struct LdsCtx {
 
 __device__ __forceinline__ uint32_t* lds_u32() { return reinterpret_cast<uint32_t*>(g_lds); }
 
-// MRT_WOOP builds (A/B): the all-in-LDS leaf triangles as unit-triangle
-// records (mrt_layout.h DeviceScene::wtris, 4 float4 each)
-#ifndef MRT_WOOP
-#define MRT_WOOP 0
-#endif
-constexpr uint32_t kTriF4 = MRT_WOOP ? 4u : 3u;
 // float4s per staged node: the all-in-LDS BVH4 stages four
 // quadrant copies of the six plane rows and the refs row (consecutive copies
 // start 28 banks apart, so lanes of different quadrants reading the same node
@@ -331,7 +307,7 @@ __host__ __device__ constexpr uint32_t node_stride_f4(int mode, uint32_t node_f4
 __host__ __device__ inline uint32_t lds_scene_float4s(int mode, uint32_t node_f4, uint32_t nodes, uint32_t lds_nodes,
                                                       uint32_t tri_records, uint32_t prims, uint32_t mats,
                                                       uint32_t lights) {
-  if (mode == kAllLds) return node_stride_f4(mode, node_f4) * nodes + kTriF4 * tri_records + 6 * prims + 2 * mats + 7 * lights;
+  if (mode == kAllLds) return node_stride_f4(mode, node_f4) * nodes + 3 * tri_records + 6 * prims + 2 * mats + 7 * lights;
   if (mode == kTopLds) return node_f4 * lds_nodes;
   return 0;
 }
@@ -458,7 +434,7 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   const uint32_t node_f4 = node_stride_f4(MODE, nf4);
   const bool copies = node_f4 != nf4;
   cx.tri_base = node_f4 * n_nodes;
-  cx.prim_base = cx.tri_base + (MODE == kAllLds ? kTriF4 : 3u) * TR;
+  cx.prim_base = cx.tri_base + 3 * TR;
   cx.mat_base = cx.prim_base + 6 * T;
   cx.light_base = cx.mat_base + 2 * M;
   const uint32_t f4 = cx.light_base + 7 * NL;
@@ -467,12 +443,11 @@ __device__ __forceinline__ LdsCtx stage_lds(const DeviceScene& sc, uint32_t scra
   cx.spill_lane = sc.max_stack;
   cx.spill = spill ? spill + (size_t)blockIdx.x * kBlock * cx.spill_lane : nullptr;
   if (MODE != kGlobal) {
-    const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes),
-                            reinterpret_cast<const float4*>(MRT_WOOP && MODE == kAllLds ? sc.wtris : sc.tris),
+    const float4* src[5] = {reinterpret_cast<const float4*>(sc.nodes), reinterpret_cast<const float4*>(sc.tris),
                             reinterpret_cast<const float4*>(sc.prims), reinterpret_cast<const float4*>(sc.materials),
                             reinterpret_cast<const float4*>(sc.lights)};
     const uint32_t base[5] = {0u, cx.tri_base, cx.prim_base, cx.mat_base, cx.light_base};
-    const uint32_t len[5] = {nf4 * n_nodes, (MODE == kAllLds ? kTriF4 : 3u) * TR, 6 * T, 2 * M, 7 * NL};
+    const uint32_t len[5] = {nf4 * n_nodes, 3 * TR, 6 * T, 2 * M, 7 * NL};
     for (int r = copies ? 1 : 0; r < 5; ++r)
       for (uint32_t i = threadIdx.x; i < len[r]; i += kBlock) g_lds[base[r] + i] = src[r][i];
     if (copies) {   // quadrant copies: x, y rows (near, far), z rows (lo, hi), refs
@@ -669,25 +644,14 @@ template <int MODE>
 __device__ __forceinline__ bool tri_pair(const DeviceScene& sc, const LdsCtx& cx, V3 o, V3 d, float tmin,
                                          uint32_t ka, uint32_t kb, bool pair, Hit& h, bool any, uint32_t target,
                                          uint32_t* uv) {
+  float4 a0, a1, a2, b0, b1, b2;
+  fetch_tri<MODE>(sc, cx, ka, a0, a1, a2);
+  fetch_tri<MODE>(sc, cx, kb, b0, b1, b2);
   float t[2], u[2], v[2];
   bool ok[2];
-  uint32_t prim[2];
-  if (MRT_WOOP && MODE == kAllLds) {
-    const float4 a0 = g_lds[cx.tri_base + 4 * ka], a1 = g_lds[cx.tri_base + 4 * ka + 1], a2 = g_lds[cx.tri_base + 4 * ka + 2];
-    const float4 b0 = g_lds[cx.tri_base + 4 * kb], b1 = g_lds[cx.tri_base + 4 * kb + 1], b2 = g_lds[cx.tri_base + 4 * kb + 2];
-    prim[0] = fbits(g_lds[cx.tri_base + 4 * ka + 3].x);
-    prim[1] = fbits(g_lds[cx.tri_base + 4 * kb + 3].x);
-    ok[0] = tri_woop(o, d, a0, a1, a2, t[0], u[0], v[0]);
-    ok[1] = tri_woop(o, d, b0, b1, b2, t[1], u[1], v[1]) & pair;
-  } else {
-    float4 a0, a1, a2, b0, b1, b2;
-    fetch_tri<MODE>(sc, cx, ka, a0, a1, a2);
-    fetch_tri<MODE>(sc, cx, kb, b0, b1, b2);
-    ok[0] = tri_bary(o, d, mk(a0), mk(a1), mk(a2), t[0], u[0], v[0]);
-    ok[1] = tri_bary(o, d, mk(b0), mk(b1), mk(b2), t[1], u[1], v[1]) & pair;
-    prim[0] = fbits(a0.w);
-    prim[1] = fbits(b0.w);
-  }
+  ok[0] = tri_bary(o, d, mk(a0), mk(a1), mk(a2), t[0], u[0], v[0]);
+  ok[1] = tri_bary(o, d, mk(b0), mk(b1), mk(b2), t[1], u[1], v[1]) & pair;
+  const uint32_t prim[2] = {fbits(a0.w), fbits(b0.w)};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const bool hit = ok[j] & (t[j] >= tmin) & (t[j] <= h.t);

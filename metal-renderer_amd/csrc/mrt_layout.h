@@ -86,8 +86,6 @@ constexpr uint32_t kIntersectSpillGrid = 1024;      // persistent grid of the st
 struct DeviceScene {
   const float* nodes;        // float4 x 8 per BVH4 node (see above)
   const float* tris;         // float4 x 3 per leaf-ordered triangle: (v0, bits(prim)), (e1, 0), (e2, 0)
-  const float* wtris;        // float4 x 4 per leaf-ordered triangle (MRT_WOOP builds, A/B): the rows of the
-                             //   world -> unit-triangle transform (m_i, -m_i . v0), then (bits(prim), 0, 0, 0)
   const float* prims;        // float4 x 6 per primitive (original order):
                              //   (p0, bits(material)), (p1, bits(light index or ~0u)), (p2, 0),
                              //   (n0, 0), (n1, 0), (n2, 0)

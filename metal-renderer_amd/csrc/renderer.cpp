@@ -111,7 +111,7 @@ struct mrt_scene {
   std::vector<uint32_t> occ_keep;   // primitives the occluder tree holds
   int32_t occ_root = 0;
   uint32_t occ_node_base = 0, occ_max_stack = 0;
-  DevBuf nodes, tris, wtris, prims, materials, lights;
+  DevBuf nodes, tris, prims, materials, lights;
   mrt::DeviceScene dev{};
   mrt_scene_info info{};
 };
@@ -764,40 +764,6 @@ int mrt_noise_table(uint64_t seed, int64_t frame, float* out) {
 // ---------------------------------------------------------------------------
 // scene
 // ---------------------------------------------------------------------------
-// Unit-triangle (Woop) records of the leaf triangles for MRT_WOOP builds
-// (A/B): rows of the inverse of [e1 e2 n] with the translation -m . v0.
-static std::vector<float> woop_records(const std::vector<float>& tris) {
-  const size_t n = tris.size() / 12;
-  std::vector<float> w(16 * n, 0.0f);
-  for (size_t i = 0; i < n; ++i) {
-    const float* r = &tris[12 * i];
-    const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[4], r[5], r[6]}, e2[3] = {r[8], r[9], r[10]};
-    auto cross = [](const double* a, const double* b, double* c) {
-      c[0] = a[1] * b[2] - a[2] * b[1]; c[1] = a[2] * b[0] - a[0] * b[2]; c[2] = a[0] * b[1] - a[1] * b[0];
-    };
-    double nn[3], c12[3], c20[3], c01[3];
-    cross(e1, e2, nn);
-    cross(e2, nn, c12);
-    cross(nn, e1, c20);
-    cross(e1, e2, c01);
-    const double det = e1[0] * c12[0] + e1[1] * c12[1] + e1[2] * c12[2];
-    float* o = &w[16 * i];
-    if (!(std::fabs(det) > 0.0)) {   // degenerate: never hit (dz = 0)
-      o[11] = 1.0f;
-    } else {
-      const double* rows[3] = {c12, c20, c01};
-      for (int k = 0; k < 3; ++k) {
-        double m[3] = {rows[k][0] / det, rows[k][1] / det, rows[k][2] / det};
-        if (k == 2) { const double nd = nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]; for (int c = 0; c < 3; ++c) m[c] = nn[c] / nd; }
-        for (int c = 0; c < 3; ++c) o[4 * k + c] = (float)m[c];
-        o[4 * k + 3] = (float)(-(m[0] * v0[0] + m[1] * v0[1] + m[2] * v0[2]));
-      }
-    }
-    std::memcpy(&o[12], &r[3], 4);   // the primitive id
-  }
-  return w;
-}
-
 int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (!desc || !out || !desc->obj_path) return fail(MRT_ERR_INVALID, "mrt_scene_create: null argument");
   *out = nullptr;
@@ -1060,10 +1026,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   if (builder == MRT_BVH_HOST_SAH) {
     HIP_TRY(upload(s->nodes, up_nodes.data(), up_nodes.size() * 4));
     HIP_TRY(upload(s->tris, up_tris.data(), up_tris.size() * 4));
-    if (T < 65536) {
-      const std::vector<float> wt = woop_records(up_tris);
-      HIP_TRY(upload(s->wtris, wt.data(), wt.size() * 4));
-    }
   }
   HIP_TRY(upload(s->prims, prims.data(), prims.size() * 4));
   HIP_TRY(upload(s->materials, mats.data(), mats.size() * 4));
@@ -1071,7 +1033,6 @@ int mrt_scene_create(const mrt_scene_desc* desc, mrt_scene** out) {
   mrt::DeviceScene& d = s->dev;
   d.nodes = s->nodes.as<float>();
   d.tris = s->tris.as<float>();
-  d.wtris = s->wtris.bytes ? s->wtris.as<float>() : nullptr;
   d.prims = s->prims.as<float>();
   d.materials = s->materials.as<float>();
   d.lights = s->lights.as<float>();
